@@ -1,0 +1,213 @@
+/*
+ * sctools_gpu.h -- C-ABI of libsctools_gpu.so, the MI355X (gfx950) metric engine.
+ *
+ * This is the drop-in boundary for the reference's per-record Python hot loop.
+ * Every entry point below names the reference interface it replaces
+ * (file:line into fredlas/sctools, src/sctools/...).  The reference has no
+ * native FFI for this path; the binding a maintainer would
+ * add on the reference side is a ctypes stub, shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Record columns, workspace, partials and
+ *     outputs are DEVICE pointers (hipMalloc / torch CUDA tensors) unless a
+ *     parameter says "host".  `stream` is a hipStream_t passed as void*
+ *     (NULL = the legacy default stream).
+ *   - The library never allocates or frees caller memory.  Workspace is
+ *     caller-provided and sized by sct_workspace_size().
+ *   - Return 0 on success, a negative SCT_E* code on failure; the message is
+ *     available from sct_last_error() (thread-local).
+ *   - Reentrant: one call per (device, stream) at a time; no global mutable
+ *     state besides the thread-local error string.
+ */
+#ifndef SCTOOLS_GPU_H
+#define SCTOOLS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCT_ABI_VERSION 1
+
+/* ---- error codes ---- */
+#define SCT_OK 0
+#define SCT_EINVAL (-1)  /* bad argument / shape */
+#define SCT_EHIP (-2)    /* HIP runtime error */
+#define SCT_ENOMEM (-3)  /* workspace too small */
+#define SCT_ENCCL (-4)   /* RCCL error */
+
+/* ---- per-record columns: the 32-byte SoA record ----
+ * Read by the reference per record in MetricAggregator.parse_molecule
+ * (metrics/aggregator.py:251-334) and CellMetrics.parse_extra_fields
+ * (metrics/aggregator.py:507-530). */
+#define SCT_B_UNMAPPED 0x01u     /* flag & 0x4                       */
+#define SCT_B_REVERSE 0x02u      /* flag & 0x10                      */
+#define SCT_B_DUPLICATE 0x04u    /* flag & 0x400                     */
+#define SCT_B_SPLICED 0x08u      /* CIGAR N length > 0               */
+#define SCT_B_NH1 0x10u          /* NH == 1                          */
+#define SCT_B_PERFECT_UMI 0x20u  /* UR and UB present, UR == UB      */
+#define SCT_B_HAS_CB 0x40u       /* CB present                       */
+#define SCT_B_PERFECT_CB 0x80u   /* CB present, CR == CB             */
+
+#define SCT_XF_ABSENT 0
+#define SCT_XF_CODING 1
+#define SCT_XF_INTRONIC 2
+#define SCT_XF_UTR 3
+#define SCT_XF_INTERGENIC 4
+#define SCT_XF_OTHER 5
+
+typedef struct sct_records {
+  int64_t n;                /* number of records                              */
+  const int32_t* cell;      /* CB dictionary id (missing CB is an id)         */
+  const int32_t* umi;       /* UB dictionary id                               */
+  const int32_t* gene;      /* GE dictionary id                               */
+  const int32_t* ref;       /* reference_id                                   */
+  const int32_t* pos;       /* 0-based leftmost position                      */
+  const uint16_t* gq_sum;   /* sum(query_alignment_qualities)                 */
+  const uint16_t* gq_len;   /* len(query_alignment_qualities)                 */
+  const uint16_t* gq_gt30;  /* #query_alignment_qualities > 30                */
+  const uint8_t* bits;      /* SCT_B_*                                        */
+  const uint8_t* xf;        /* SCT_XF_*                                       */
+  const uint8_t* cy_gt30;   /* #CY phred > 30                                 */
+  const uint8_t* cy_len;    /* len(CY)                                        */
+  const uint8_t* uy_gt30;   /* #UY phred > 30                                 */
+  const uint8_t* uy_len;    /* len(UY)                                        */
+} sct_records_t;
+
+/* ---- what an entity is ---- */
+#define SCT_MODE_CELL 0         /* maximal run of equal `cell` (GatherCellMetrics, gatherer.py:116-159) */
+#define SCT_MODE_GENE 1         /* maximal run of equal `gene` (GatherGeneMetrics, gatherer.py:189-232) */
+#define SCT_MODE_GENE_GROUPED 2 /* every record of a gene id: per-gene partials, additive across
+                                   cell shards; replaces MergeGeneMetrics (merge.py:74-191)          */
+
+/* ---- how mean / variance are computed ---- */
+#define SCT_FLOAT_EXACT_SUM 0 /* order-free exact fixed-point sums (x * 2^68 is an integer),
+                                 correctly rounded mean and variance; independent of order,
+                                 tiling and GPU count; within 1e-12 relative of Welford           */
+#define SCT_FLOAT_WELFORD 1   /* sequential Welford in record order (stats.py:82-99): bit-identical
+                                 to the reference; RUN modes only                                 */
+
+typedef struct sct_plan {
+  int64_t n_records;
+  int64_t max_entities; /* upper bound on RUN-mode rows (from sct_count_entities);
+                           0 = n_records.  Sizes the workspace.           */
+  int32_t mode;         /* SCT_MODE_*                                     */
+  int32_t float_mode;   /* SCT_FLOAT_*                                    */
+  int32_t n_cell_ids;   /* dictionary sizes: ids are in [0, n_*_ids)      */
+  int32_t n_gene_ids;
+  int32_t n_umi_ids;
+  int32_t reserved;
+} sct_plan_t;
+
+/* ---- output rows ----
+ * ints [rows][SCT_NI] (int64) and floats [rows][SCT_NF] (double).  Column
+ * names follow the reference header (MetricAggregator.__init__,
+ * aggregator.py:132-189; CellMetrics 437-461; GeneMetrics 561-569). */
+#define SCT_NI 24
+#define SCT_I_N_READS 0
+#define SCT_I_NOISE_READS 1 /* always 0 (not implemented by the reference either) */
+#define SCT_I_PERFECT_MOLECULE_BARCODES 2
+#define SCT_I_READS_MAPPED_EXONIC 3
+#define SCT_I_READS_MAPPED_INTRONIC 4
+#define SCT_I_READS_MAPPED_UTR 5
+#define SCT_I_READS_MAPPED_UNIQUELY 6
+#define SCT_I_READS_MAPPED_MULTIPLE 7
+#define SCT_I_DUPLICATE_READS 8
+#define SCT_I_SPLICED_READS 9
+#define SCT_I_ANTISENSE_READS 10 /* always 0 */
+#define SCT_I_N_MOLECULES 11
+#define SCT_I_N_FRAGMENTS 12
+#define SCT_I_FRAGMENTS_SINGLE 13
+#define SCT_I_MOLECULES_SINGLE 14
+#define SCT_I_PERFECT_CELL_BARCODES 15 /* cell */
+#define SCT_I_READS_MAPPED_INTERGENIC 16 /* cell */
+#define SCT_I_READS_UNMAPPED 17 /* cell */
+#define SCT_I_READS_TOO_MANY_LOCI 18 /* always 0 */
+#define SCT_I_N_K1 19        /* cell: n_genes; gene: number_cells_expressing */
+#define SCT_I_K1_MULTIPLE 20 /* cell: genes_detected_multiple_observations; gene: number_cells_detected_multiple */
+#define SCT_I_N_MITO_GENES 21 /* cell */
+#define SCT_I_N_MITO_MOLECULES 22 /* cell (counts reads, as the reference does) */
+#define SCT_I_ENTITY 23       /* RUN modes: index of the entity's first record; GROUPED: gene id */
+
+#define SCT_NF 12
+#define SCT_F_UY_MEAN 0 /* molecule_barcode_fraction_bases_above_30_mean */
+#define SCT_F_UY_VAR 1
+#define SCT_F_GQF_MEAN 2 /* genomic_reads_fraction_bases_quality_above_30_mean */
+#define SCT_F_GQF_VAR 3
+#define SCT_F_GQ_MEAN 4 /* genomic_read_quality_mean */
+#define SCT_F_GQ_VAR 5
+#define SCT_F_READS_PER_MOLECULE 6
+#define SCT_F_READS_PER_FRAGMENT 7
+#define SCT_F_FRAGMENTS_PER_MOLECULE 8
+#define SCT_F_CY_VAR 9 /* cell_barcode_fraction_bases_above_30_variance */
+#define SCT_F_CY_MEAN 10
+#define SCT_F_PCT_MITO 11
+
+/* ---- additive partials (GROUPED mode; also the internal RUN-mode row state) ----
+ * int64 [rows][SCT_NP]: 24 counter slots, then per float stream (UY frac,
+ * genomic frac, genomic mean quality, CY frac) 3 lanes of sum(x*2^68) and 5
+ * lanes of sum((x*2^68)^2); a lane holds a sum of 32-bit limb values, so
+ * lanes are plain int64 sums and partials of disjoint record sets add
+ * lane-wise (this is what the RCCL all-reduce sums).  Slot 20 of a RUN-mode
+ * row holds the entity's first record index and is not additive. */
+#define SCT_NP 64
+#define SCT_P_FLOAT_BASE 24
+#define SCT_P_STREAM_LANES 8
+
+/* ABI version of the loaded library (== SCT_ABI_VERSION). */
+int sct_abi_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* sct_last_error(void);
+
+/* Device workspace bytes needed for `plan`. */
+int sct_workspace_size(const sct_plan_t* plan, size_t* bytes);
+
+/* Number of output rows for `plan` (RUN modes: entity runs; GROUPED:
+ * n_gene_ids).  Replaces the entity enumeration of bam.iter_tag_groups
+ * (bam.py:492-540).  Synchronizes `stream`. */
+int sct_count_entities(const sct_plan_t* plan, const sct_records_t* rec, void* workspace,
+                       size_t workspace_bytes, int64_t* n_entities /* host */, void* stream);
+
+/* Full metric rows for RUN modes (cell or gene entities, file order).
+ * Replaces GatherCellMetrics.extract_metrics / GatherGeneMetrics.extract_metrics'
+ * aggregation (gatherer.py:134-159 / 207-232): MetricAggregator.parse_molecule
+ * (aggregator.py:236-334), parse_extra_fields (492-530, 580-595) and finalize
+ * (342-387, 463-490, 571-578).  `gene_is_mito`/`gene_is_multi` are device
+ * uint8[n_gene_ids].  `out_ints`/`out_floats` hold `capacity` rows; the row
+ * count is returned in *n_rows (host).  Gene rows of multi-gene runs are
+ * computed like any other; the caller drops them (gatherer.py:210-212). */
+int sct_compute_metrics(const sct_plan_t* plan, const sct_records_t* rec,
+                        const uint8_t* gene_is_mito, const uint8_t* gene_is_multi,
+                        void* workspace, size_t workspace_bytes, int64_t* out_ints,
+                        double* out_floats, int64_t capacity, int64_t* n_rows /* host */,
+                        void* stream);
+
+/* Per-gene additive partials (GROUPED mode) of this rank's records, written
+ * to `partials` [n_gene_ids][SCT_NP] (overwritten).  Records must be
+ * cell-sharded (no cell run split across calls), the SplitBam invariant
+ * (bam.py:439-448). */
+int sct_gene_partials(const sct_plan_t* plan, const sct_records_t* rec, void* workspace,
+                      size_t workspace_bytes, int64_t* partials, void* stream);
+
+/* Finalize `rows` partial rows into output rows (floats and ratios; the
+ * reference's finalize(), aggregator.py:342-387, 463-490, 571-578).  `mode`
+ * selects cell or gene columns; entity ids are written as the row index. */
+int sct_finalize_partials(int32_t mode, const int64_t* partials, int64_t rows, int64_t* out_ints,
+                          double* out_floats, void* stream);
+
+/* Optional kernel timing: while enabled, every kernel launch is bracketed by
+ * HIP events on its launch stream.  sct_profile_read waits for the events,
+ * fills up to `max_kernels` (name, total ms, launches) triples (host arrays;
+ * names stay valid until the next read), resets, and returns the number of
+ * distinct kernels seen.  Thread-local. */
+int sct_profile_enable(int on);
+int sct_profile_read(const char** names, double* ms, int64_t* launches, int max_kernels);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SCTOOLS_GPU_H */

@@ -1,0 +1,329 @@
+"""
+Minimal BAM / SAM record reader (host side).
+
+The reference reads alignments through ``pysam`` (``pysam==0.16.0.1``,
+``/root/reference/requirements.txt:3``), which is not installed in this image.
+This module is a self-contained reader for the subset of the SAM/BAM spec the
+metric path touches: the fixed BAM core fields, the CIGAR, the base qualities
+and the optional tags.  It reproduces the pysam 0.16 semantics that the
+reference's ``MetricAggregator.parse_molecule`` depends on
+(``/root/reference/src/sctools/metrics/aggregator.py:251-334``):
+
+* ``query_alignment_qualities``: qualities between the leading and trailing
+  soft clips (pysam ``getQueryStart`` / ``getQueryEnd``; hard clips skipped,
+  the trailing walk stops at CIGAR index 1), ``None`` when the read has no
+  sequence or its first quality byte is 0xff;
+* ``get_cigar_stats()[0][3]``: the summed length of ``N`` operations;
+* ``get_tag``: ``KeyError`` for an absent tag.
+
+BGZF is a concatenation of gzip members, so it is inflated with ``zlib`` in
+streaming fashion.  A native multi-threaded decoder is the SURVEY §8(f) #1
+follow-up; this reader is what the fixtures and the drop-in API use today.
+"""
+
+import struct
+import zlib
+from typing import Dict, Iterator, List, Optional, Tuple
+
+__all__ = ["BamRecord", "open_alignments", "read_header"]
+
+_CIGAR_OPS = "MIDNSHP=X"
+_SEQ_NT16 = "=ACMGRSVTWYHKDBN"
+
+BAM_CMATCH, BAM_CINS, BAM_CDEL, BAM_CREF_SKIP, BAM_CSOFT_CLIP, BAM_CHARD_CLIP = range(6)
+BAM_CEQUAL, BAM_CDIFF = 7, 8
+
+_TAG_INT_FMT = {"c": "<b", "C": "<B", "s": "<h", "S": "<H", "i": "<i", "I": "<I"}
+_ARRAY_FMT = {"c": "b", "C": "B", "s": "h", "S": "H", "i": "i", "I": "I", "f": "f"}
+
+
+class BamRecord:
+    """One alignment with the attributes the metric path reads.
+
+    Attribute names follow ``pysam.AlignedSegment`` so the host code reads
+    like the reference.
+    """
+
+    __slots__ = (
+        "query_name", "flag", "reference_id", "pos", "mapq", "cigar",
+        "l_seq", "_qual", "_tags",
+    )
+
+    def __init__(self, query_name, flag, reference_id, pos, mapq, cigar, l_seq, qual, tags):
+        self.query_name = query_name
+        self.flag = flag
+        self.reference_id = reference_id
+        self.pos = pos
+        self.mapq = mapq
+        self.cigar = cigar  # list of (op, length)
+        self.l_seq = l_seq
+        self._qual = qual  # bytes (raw phred, 0xff.. if absent) or None
+        self._tags = tags  # dict tag -> python value
+
+    # --- flag helpers (pysam names) ---
+    @property
+    def is_unmapped(self) -> bool:
+        return bool(self.flag & 0x4)
+
+    @property
+    def is_reverse(self) -> bool:
+        return bool(self.flag & 0x10)
+
+    @property
+    def is_duplicate(self) -> bool:
+        return bool(self.flag & 0x400)
+
+    @property
+    def is_secondary(self) -> bool:
+        return bool(self.flag & 0x100)
+
+    # --- tags ---
+    def get_tag(self, tag: str):
+        return self._tags[tag]
+
+    def has_tag(self, tag: str) -> bool:
+        return tag in self._tags
+
+    def get_tags(self):
+        return list(self._tags.items())
+
+    # --- CIGAR derived ---
+    def n_skip_length(self) -> int:
+        """Summed length of N (reference skip) operations: pysam ``get_cigar_stats()[0][3]``."""
+        return sum(length for op, length in self.cigar if op == BAM_CREF_SKIP)
+
+    def query_start(self) -> int:
+        """pysam 0.16 ``getQueryStart``: leading soft clips, hard clips skipped."""
+        start = 0
+        for op, length in self.cigar:
+            if op == BAM_CHARD_CLIP:
+                if start != 0 and start != self.l_seq:
+                    raise ValueError("Invalid clipping in CIGAR string")
+            elif op == BAM_CSOFT_CLIP:
+                start += length
+            else:
+                break
+        return start
+
+    def query_end(self) -> int:
+        """pysam 0.16 ``getQueryEnd``: l_seq minus trailing soft clips (walk stops at index 1)."""
+        end = self.l_seq
+        if end == 0:
+            for op, length in self.cigar:
+                if op in (BAM_CMATCH, BAM_CINS, BAM_CEQUAL, BAM_CDIFF) or (
+                    op == BAM_CSOFT_CLIP and end == 0
+                ):
+                    end += length
+            return end
+        for k in range(len(self.cigar) - 1, 0, -1):
+            op, length = self.cigar[k]
+            if op == BAM_CHARD_CLIP:
+                if end != self.l_seq:
+                    raise ValueError("Invalid clipping in CIGAR string")
+            elif op == BAM_CSOFT_CLIP:
+                end -= length
+            else:
+                break
+        return end
+
+    @property
+    def query_alignment_qualities(self) -> Optional[bytes]:
+        if self.l_seq == 0 or self._qual is None:
+            return None
+        if len(self._qual) == 0 or self._qual[0] == 0xFF:
+            return None
+        start, end = self.query_start(), self.query_end()
+        if end < start:
+            return b""
+        return self._qual[start:end]
+
+
+def _parse_tags(buf: bytes, off: int, end: int) -> Dict[str, object]:
+    tags = {}
+    unpack_from = struct.unpack_from
+    while off < end:
+        tag = buf[off:off + 2].decode("ascii")
+        typ = chr(buf[off + 2])
+        off += 3
+        if typ == "Z" or typ == "H":
+            nul = buf.index(b"\x00", off)
+            tags[tag] = buf[off:nul].decode("ascii", "replace")
+            off = nul + 1
+        elif typ in _TAG_INT_FMT:
+            fmt = _TAG_INT_FMT[typ]
+            tags[tag] = unpack_from(fmt, buf, off)[0]
+            off += struct.calcsize(fmt)
+        elif typ == "A":
+            tags[tag] = chr(buf[off])
+            off += 1
+        elif typ == "f":
+            tags[tag] = unpack_from("<f", buf, off)[0]
+            off += 4
+        elif typ == "d":
+            tags[tag] = unpack_from("<d", buf, off)[0]
+            off += 8
+        elif typ == "B":
+            sub = chr(buf[off])
+            count = unpack_from("<i", buf, off + 1)[0]
+            off += 5
+            code = _ARRAY_FMT[sub]
+            size = struct.calcsize(code)
+            tags[tag] = list(struct.unpack_from("<%d%s" % (count, code), buf, off))
+            off += count * size
+        else:
+            raise ValueError("unsupported BAM tag type %r" % typ)
+    return tags
+
+
+class _BgzfStream:
+    """Streaming inflater over concatenated gzip members (BGZF)."""
+
+    def __init__(self, path: str, chunk: int = 1 << 20):
+        self._fh = open(path, "rb")
+        self._chunk = chunk
+        self._buf = bytearray()
+        self._pos = 0
+        self._d = zlib.decompressobj(16 + zlib.MAX_WBITS)
+        self._eof = False
+
+    def close(self):
+        self._fh.close()
+
+    def _fill(self, need: int) -> None:
+        while len(self._buf) - self._pos < need and not self._eof:
+            raw = self._fh.read(self._chunk)
+            if not raw:
+                self._eof = True
+                break
+            while raw:
+                out = self._d.decompress(raw)
+                self._buf += out
+                if self._d.eof:
+                    raw = self._d.unused_data
+                    self._d = zlib.decompressobj(16 + zlib.MAX_WBITS)
+                else:
+                    raw = b""
+        if self._pos > (1 << 22):
+            del self._buf[: self._pos]
+            self._pos = 0
+
+    def read(self, n: int) -> bytes:
+        self._fill(n)
+        out = bytes(self._buf[self._pos:self._pos + n])
+        self._pos += len(out)
+        return out
+
+
+def _iter_bam(path: str) -> Iterator[BamRecord]:
+    stream = _BgzfStream(path)
+    try:
+        magic = stream.read(4)
+        if magic != b"BAM\x01":
+            raise ValueError("%s is not a BAM file" % path)
+        (l_text,) = struct.unpack("<i", stream.read(4))
+        stream.read(l_text)
+        (n_ref,) = struct.unpack("<i", stream.read(4))
+        for _ in range(n_ref):
+            (l_name,) = struct.unpack("<i", stream.read(4))
+            stream.read(l_name + 4)
+        core = struct.Struct("<iiBBHHHiiii")
+        while True:
+            head = stream.read(4)
+            if len(head) < 4:
+                return
+            (block_size,) = struct.unpack("<i", head)
+            data = stream.read(block_size)
+            (ref_id, pos, l_read_name, mapq, _bin, n_cigar, flag, l_seq,
+             _nref, _npos, _tlen) = core.unpack_from(data, 0)
+            off = 32
+            qname = data[off:off + l_read_name - 1].decode("ascii", "replace")
+            off += l_read_name
+            cigar = []
+            for k in range(n_cigar):
+                (c,) = struct.unpack_from("<I", data, off + 4 * k)
+                cigar.append((c & 0xF, c >> 4))
+            off += 4 * n_cigar
+            off += (l_seq + 1) // 2
+            qual = data[off:off + l_seq]
+            off += l_seq
+            tags = _parse_tags(data, off, len(data))
+            yield BamRecord(qname, flag, ref_id, pos, mapq, cigar, l_seq, qual, tags)
+    finally:
+        stream.close()
+
+
+def _parse_sam_tag(field: str):
+    tag, typ, val = field.split(":", 2)
+    if typ == "i":
+        return tag, int(val)
+    if typ == "f":
+        return tag, float(val)
+    if typ == "B":
+        parts = val.split(",")
+        conv = float if parts[0] == "f" else int
+        return tag, [conv(p) for p in parts[1:]]
+    return tag, val
+
+
+def _iter_sam(path: str) -> Iterator[BamRecord]:
+    import re
+
+    refs: Dict[str, int] = {}
+    cig_re = re.compile(r"(\d+)([MIDNSHP=X])")
+    opener = open
+    if path.endswith(".gz"):
+        import gzip
+
+        opener = gzip.open
+    with opener(path, "rt") as fh:
+        for line in fh:
+            if line.startswith("@"):
+                if line.startswith("@SQ"):
+                    for f in line.rstrip("\n").split("\t"):
+                        if f.startswith("SN:"):
+                            refs[f[3:]] = len(refs)
+                continue
+            f = line.rstrip("\n").split("\t")
+            if len(f) < 11:
+                continue
+            flag = int(f[1])
+            ref_id = refs.get(f[2], -1) if f[2] != "*" else -1
+            pos = int(f[3]) - 1
+            cigar: List[Tuple[int, int]] = []
+            if f[5] != "*":
+                cigar = [(_CIGAR_OPS.index(o), int(n)) for n, o in cig_re.findall(f[5])]
+            seq = f[9]
+            l_seq = 0 if seq == "*" else len(seq)
+            if f[10] == "*":
+                qual = b"\xff" * l_seq if l_seq else b""
+            else:
+                qual = bytes(ord(c) - 33 for c in f[10])
+            tags = dict(_parse_sam_tag(t) for t in f[11:])
+            yield BamRecord(f[0], flag, ref_id, pos, int(f[4]), cigar, l_seq, qual, tags)
+
+
+def open_alignments(path: str, mode: str = "rb") -> Iterator[BamRecord]:
+    """Iterate alignments of a BAM (``mode='rb'``) or SAM (``mode='r'``) file in file order."""
+    if "b" in mode:
+        return _iter_bam(path)
+    return _iter_sam(path)
+
+
+def read_header(path: str) -> Tuple[str, List[Tuple[str, int]]]:
+    """Return (header text, [(reference name, length)]) of a BAM file."""
+    stream = _BgzfStream(path)
+    try:
+        if stream.read(4) != b"BAM\x01":
+            raise ValueError("%s is not a BAM file" % path)
+        (l_text,) = struct.unpack("<i", stream.read(4))
+        text = stream.read(l_text).decode("ascii", "replace").rstrip("\x00")
+        (n_ref,) = struct.unpack("<i", stream.read(4))
+        refs = []
+        for _ in range(n_ref):
+            (l_name,) = struct.unpack("<i", stream.read(4))
+            name = stream.read(l_name).rstrip(b"\x00").decode("ascii")
+            (l_ref,) = struct.unpack("<i", stream.read(4))
+            refs.append((name, l_ref))
+        return text, refs
+    finally:
+        stream.close()

@@ -1,0 +1,184 @@
+"""
+Device-side driver of the HIP metric engine.
+
+Owns the plumbing around the C-ABI of ``include/sctools_gpu.h``: device
+buffers (torch CUDA tensors on ROCm), the workspace, and the stream.  All
+metric arithmetic happens in the HIP kernels of ``sctools_amd/csrc``; this
+module never computes a metric itself and has no CPU fallback: without a GPU
+or without ``libsctools_gpu.so`` it raises.
+"""
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from sctools_amd import _native as N
+
+_TORCH_DTYPES = {
+    "cell": torch.int32, "umi": torch.int32, "gene": torch.int32, "ref": torch.int32, "pos": torch.int32,
+    "gq_sum": torch.int16, "gq_len": torch.int16, "gq_gt30": torch.int16,  # uint16 bit patterns
+    "bits": torch.uint8, "xf": torch.uint8, "cy_gt30": torch.uint8, "cy_len": torch.uint8,
+    "uy_gt30": torch.uint8, "uy_len": torch.uint8,
+}
+
+MODES = {"cell": N.MODE_CELL, "gene": N.MODE_GENE, "gene_grouped": N.MODE_GENE_GROUPED}
+FLOAT_MODES = {"exact": N.FLOAT_EXACT_SUM, "welford": N.FLOAT_WELFORD}
+
+
+def _device(device=None) -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("sctools_amd needs a ROCm GPU (torch.cuda.is_available() is False); "
+                           "there is no CPU fallback")
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device(device)
+
+
+def to_device(arrays: Dict[str, np.ndarray], device=None) -> Dict[str, torch.Tensor]:
+    """Copy host columns (numpy) to device tensors of the engine's dtypes."""
+    dev = _device(device)
+    out = {}
+    for c in N.RECORD_COLUMNS:
+        a = np.ascontiguousarray(arrays[c])
+        t = _TORCH_DTYPES[c]
+        if t == torch.int16:
+            a = a.astype(np.uint16, copy=False).view(np.int16)
+        out[c] = torch.from_numpy(a).to(dev, non_blocking=False)
+    return out
+
+
+def records_struct(cols: Dict[str, torch.Tensor]) -> N.Records:
+    n = int(cols["cell"].numel())
+    r = N.Records()
+    r.n = n
+    for c in N.RECORD_COLUMNS:
+        t = cols[c]
+        if t.numel() != n:
+            raise ValueError("column %s has %d records, expected %d" % (c, t.numel(), n))
+        if not t.is_contiguous():
+            raise ValueError("column %s is not contiguous" % c)
+        if t.element_size() != torch.empty((), dtype=_TORCH_DTYPES[c]).element_size():
+            raise ValueError("column %s has element size %d" % (c, t.element_size()))
+        setattr(r, c, t.data_ptr() if n else None)
+    return r
+
+
+@dataclass
+class Dims:
+    n_cell_ids: int
+    n_gene_ids: int
+    n_umi_ids: int
+
+
+class Engine:
+    """One engine per device; calls are issued on torch's current stream."""
+
+    def __init__(self, device=None):
+        self.lib = N.load()
+        self.device = _device(device)
+        self._ws: Optional[torch.Tensor] = None
+
+    # ---- helpers ----
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _plan(self, n, mode, float_mode, dims: Dims, max_entities=0) -> N.Plan:
+        p = N.Plan()
+        p.n_records = int(n)
+        p.max_entities = int(max_entities)
+        p.mode = MODES[mode]
+        p.float_mode = FLOAT_MODES[float_mode]
+        p.n_cell_ids = max(1, int(dims.n_cell_ids))
+        p.n_gene_ids = max(1, int(dims.n_gene_ids))
+        p.n_umi_ids = max(1, int(dims.n_umi_ids))
+        return p
+
+    def workspace(self, plan: N.Plan) -> torch.Tensor:
+        nbytes = ctypes.c_size_t(0)
+        N.check(self.lib.sct_workspace_size(ctypes.byref(plan), ctypes.byref(nbytes)))
+        need = int(nbytes.value)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = None
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def release(self):
+        self._ws = None
+
+    # ---- entry points ----
+    def count_entities(self, cols, mode: str, dims: Dims) -> int:
+        rec = records_struct(cols)
+        plan = self._plan(rec.n, mode, "exact", dims, max_entities=1)
+        ws = self.workspace(plan)
+        out = ctypes.c_int64(0)
+        N.check(self.lib.sct_count_entities(ctypes.byref(plan), ctypes.byref(rec), ctypes.c_void_p(ws.data_ptr()),
+                                            ws.numel(), ctypes.byref(out), self._stream()))
+        return int(out.value)
+
+    def compute(self, cols, mode: str, dims: Dims, gene_is_mito: torch.Tensor, gene_is_multi: torch.Tensor,
+                float_mode: str = "exact", n_entities: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """RUN-mode rows: (ints [rows, 24] int64, floats [rows, 12] float64) on the device."""
+        if mode not in ("cell", "gene"):
+            raise ValueError("compute() handles RUN modes 'cell' and 'gene'")
+        rec = records_struct(cols)
+        if n_entities is None:
+            n_entities = self.count_entities(cols, mode, dims)
+        cap = max(1, int(n_entities))
+        plan = self._plan(rec.n, mode, float_mode, dims, max_entities=cap)
+        ws = self.workspace(plan)
+        ints = torch.empty((cap, N.SCT_NI), dtype=torch.int64, device=self.device)
+        floats = torch.empty((cap, N.SCT_NF), dtype=torch.float64, device=self.device)
+        rows = ctypes.c_int64(0)
+        N.check(self.lib.sct_compute_metrics(
+            ctypes.byref(plan), ctypes.byref(rec), ctypes.c_void_p(gene_is_mito.data_ptr()),
+            ctypes.c_void_p(gene_is_multi.data_ptr()), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+            ctypes.c_void_p(ints.data_ptr()), ctypes.c_void_p(floats.data_ptr()), cap, ctypes.byref(rows),
+            self._stream()))
+        r = int(rows.value)
+        return ints[:r], floats[:r]
+
+    def gene_partials(self, cols, dims: Dims, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """GROUPED per-gene additive partials int64 [n_gene_ids, 64] (device)."""
+        rec = records_struct(cols)
+        plan = self._plan(rec.n, "gene_grouped", "exact", dims)
+        ws = self.workspace(plan)
+        if out is None:
+            out = torch.empty((max(1, dims.n_gene_ids), N.SCT_NP), dtype=torch.int64, device=self.device)
+        N.check(self.lib.sct_gene_partials(ctypes.byref(plan), ctypes.byref(rec), ctypes.c_void_p(ws.data_ptr()),
+                                           ws.numel(), ctypes.c_void_p(out.data_ptr()), self._stream()))
+        return out
+
+    def finalize_partials(self, partials: torch.Tensor, mode: str = "gene_grouped"):
+        rows = int(partials.shape[0])
+        ints = torch.empty((max(1, rows), N.SCT_NI), dtype=torch.int64, device=self.device)
+        floats = torch.empty((max(1, rows), N.SCT_NF), dtype=torch.float64, device=self.device)
+        N.check(self.lib.sct_finalize_partials(MODES[mode], ctypes.c_void_p(partials.data_ptr()), rows,
+                                               ctypes.c_void_p(ints.data_ptr()), ctypes.c_void_p(floats.data_ptr()),
+                                               self._stream()))
+        return ints[:rows], floats[:rows]
+
+    # ---- profiling (HIP events inside the library) ----
+    def profile_enable(self, on: bool = True):
+        self.lib.sct_profile_enable(1 if on else 0)
+
+    def profile_read(self) -> Dict[str, Tuple[float, int]]:
+        cap = 64
+        names = (ctypes.c_char_p * cap)()
+        ms = (ctypes.c_double * cap)()
+        launches = (ctypes.c_int64 * cap)()
+        k = self.lib.sct_profile_read(names, ms, launches, cap)
+        return {names[i].decode(): (float(ms[i]), int(launches[i])) for i in range(min(k, cap))}
+
+
+_engines: Dict[str, Engine] = {}
+
+
+def get_engine(device=None) -> Engine:
+    dev = _device(device)
+    key = str(dev)
+    if key not in _engines:
+        _engines[key] = Engine(dev)
+    return _engines[key]

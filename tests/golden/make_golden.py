@@ -1,0 +1,200 @@
+"""
+Generate the golden fixtures under tests/golden/ by running the UNMODIFIED
+reference gatherer (``/root/reference/src/sctools``) in the build container.
+
+Run here only (the reference never leaves this container):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+What it writes (all data, no reference source):
+* ``bam/*.bam``          copies of the reference's own metric test BAMs (inputs);
+* ``ref/notebook_gene_metrics.csv``  the full-precision gene CSV embedded in
+  ``characterize-gene-testing-data.ipynb`` cell 42 (the reference's only
+  full-precision golden vector);
+* ``ref/<bam>.{cell,gene}.csv``  reference outputs for each BAM (compress=False);
+* ``synth/<set>.npz``    synthetic columnar inputs (SURVEY.md §8(d) recipe, small);
+* ``synth/<set>.{cell,gene_run,gene_grouped}.csv``  reference outputs for them.
+
+The stand-in ``pysam``/``crimson`` under ``tests/golden/stubs`` make the
+reference importable.  Before writing anything the script
+checks that the reference reproduces the notebook CSV byte-for-byte on
+``small-gene-sorted.bam``; that pins the stub's pysam semantics.
+"""
+
+import json
+import os
+import shutil
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_SRC = "/root/reference/src"
+REF_DATA = os.path.join(REF_SRC, "sctools", "test", "data")
+
+sys.dont_write_bytecode = True
+sys.path.insert(0, os.path.join(HERE, "stubs"))
+sys.path.insert(0, REPO)
+sys.path.insert(0, REF_SRC)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import pysam  # noqa: E402  (the stub)
+from sctools.metrics.gatherer import GatherCellMetrics, GatherGeneMetrics  # noqa: E402
+
+from sctools_amd import columnar as col  # noqa: E402
+from sctools_amd import synth  # noqa: E402
+
+BAMS = [
+    "small-cell-sorted.bam",
+    "small-gene-sorted.bam",
+    "cell-sorted-missing-cb.bam",
+    "unsorted.bam",
+    "cell-gene-umi-queryname-sorted.bam",
+]
+
+SYNTH_SETS = {
+    # name: (SynthConfig kwargs, within-cell shuffle seed or None)
+    "s0": (dict(n_reads=20_000, n_cells=30, n_genes=300, sigma=1.0, seed=0,
+                p_none_cell_reads=0.02), None),
+    "s1": (dict(n_reads=60_000, n_cells=120, n_genes=2_000, sigma=1.5, seed=1), None),
+    "s2": (dict(n_reads=20_000, n_cells=30, n_genes=300, sigma=1.0, seed=2,
+                p_none_cell_reads=0.01, p_unmapped=0.3, p_nh1=0.6), 7),
+    "s3": (dict(n_reads=60, n_cells=25, n_genes=12, sigma=2.0, seed=3), None),
+}
+
+
+def notebook_csv() -> str:
+    nb = json.load(open(os.path.join(REF_SRC, "sctools", "test",
+                                     "characterize-gene-testing-data.ipynb")))
+    for c in nb["cells"]:
+        for o in c.get("outputs", []):
+            t = "".join(o.get("text", []))
+            if t.startswith(",n_reads,"):
+                return t
+    raise RuntimeError("notebook golden CSV not found")
+
+
+def run_ref(gatherer, source, out_csv, **kw):
+    g = gatherer(source, out_csv[: -len(".csv")], compress=False, **kw)
+    g.extract_metrics()
+    return open(out_csv).read()
+
+
+def synth_segments(d: synth.SynthData, cols, quals):
+    """Stub AlignedSegments carrying exactly the per-record values of ``cols``."""
+    c = {k: v.numpy() for k, v in cols.items()}
+    n = c["cell"].shape[0]
+    segs = []
+    for i in range(n):
+        tags = {}
+        cname = d.cell_name(int(c["cell"][i]))
+        ub = synth.umi_string(int(c["umi"][i]))
+        gname = d.gene_names[int(c["gene"][i])]
+        bits = int(c["bits"][i])
+        if cname is not None:
+            tags["CB"] = cname
+            tags["CR"] = cname if bits & col.B_PERFECT_CB else cname[::-1] + "X"
+        tags["UB"] = ub
+        tags["UR"] = ub if bits & col.B_PERFECT_UMI else ub[::-1] + "N"
+        if gname is not None:
+            tags["GE"] = gname
+        cg, cl = int(c["cy_gt30"][i]), int(c["cy_len"][i])
+        tags["CY"] = "F" * cg + "," * (cl - cg)
+        ug, ul = int(c["uy_gt30"][i]), int(c["uy_len"][i])
+        tags["UY"] = "F" * ug + "," * (ul - ug)
+        xf = int(c["xf"][i])
+        if xf != col.XF_ABSENT:
+            tags["XF"] = {col.XF_CODING: "CODING", col.XF_INTRONIC: "INTRONIC",
+                          col.XF_UTR: "UTR", col.XF_INTERGENIC: "INTERGENIC"}[xf]
+        tags["NH"] = 1 if bits & col.B_NH1 else (0 if bits & col.B_UNMAPPED else 3)
+        flag = ((4 if bits & col.B_UNMAPPED else 0) | (16 if bits & col.B_REVERSE else 0)
+                | (1024 if bits & col.B_DUPLICATE else 0))
+        aq = quals[i, : int(c["gq_len"][i])].tolist()
+        from array import array
+
+        segs.append(pysam.AlignedSegment(tags, flag, int(c["ref"][i]), int(c["pos"][i]),
+                                         100 if bits & col.B_SPLICED else 0, array("B", aq),
+                                         "q%d" % i))
+    return segs
+
+
+def save_npz(path, d: synth.SynthData, cols):
+    arrays = {k: v.numpy() for k, v in cols.items()}
+    arrays["gq_sum"] = arrays["gq_sum"].view(np.uint16)
+    arrays["gq_len"] = arrays["gq_len"].view(np.uint16)
+    arrays["gq_gt30"] = arrays["gq_gt30"].view(np.uint16)
+    names = d.gene_names
+    arrays["gene_names"] = np.array(["" if g is None else g for g in names])
+    arrays["gene_none"] = np.array([g is None for g in names])
+    arrays["gene_is_mito"] = d.gene_is_mito
+    arrays["gene_is_multi"] = d.gene_is_multi
+    ncell = d.n_cell_ids
+    cnames = [d.cell_name(i) for i in range(ncell)]
+    arrays["cell_names"] = np.array(["" if x is None else x for x in cnames])
+    arrays["cell_none"] = np.array([x is None for x in cnames])
+    arrays["n_umi_ids"] = np.array(d.n_umi_ids)
+    np.savez_compressed(path, **arrays)
+
+
+def main():
+    os.makedirs(os.path.join(HERE, "bam"), exist_ok=True)
+    os.makedirs(os.path.join(HERE, "ref"), exist_ok=True)
+    os.makedirs(os.path.join(HERE, "synth"), exist_ok=True)
+
+    # 1. pin the stub: reference output on small-gene-sorted == notebook golden, byte for byte
+    nb = notebook_csv()
+    tmp = os.path.join(HERE, "ref", "_pin.csv")
+    got = run_ref(GatherGeneMetrics, os.path.join(REF_DATA, "small-gene-sorted.bam"), tmp)
+    os.remove(tmp)
+    assert got == nb, "stub pysam does not reproduce the notebook golden CSV"
+    with open(os.path.join(HERE, "ref", "notebook_gene_metrics.csv"), "w") as f:
+        f.write(nb)
+    print("notebook golden reproduced byte-for-byte")
+
+    # 2. reference outputs for the bundled BAMs
+    for b in BAMS:
+        shutil.copyfile(os.path.join(REF_DATA, b), os.path.join(HERE, "bam", b))
+        stem = b[: -len(".bam")]
+        src = os.path.join(REF_DATA, b)
+        run_ref(GatherCellMetrics, src, os.path.join(HERE, "ref", stem + ".cell.csv"))
+        run_ref(GatherGeneMetrics, src, os.path.join(HERE, "ref", stem + ".gene.csv"))
+        print("reference outputs for", b)
+
+    # 3. synthetic columnar sets
+    manifest = {}
+    for name, (kw, shuffle_seed) in SYNTH_SETS.items():
+        cfg = synth.SynthConfig(keep_qualities=True, **kw)
+        d = synth.generate(cfg, device="cpu")
+        cols = d.cols
+        quals = d.quals.numpy()
+        if shuffle_seed is not None:
+            # shuffle inside cells, carrying the per-base qualities along
+            n = cols["cell"].numel()
+            cols = dict(cols)
+            cols["_row"] = torch.arange(n, dtype=torch.int64)
+            cols = synth.shuffle_within_entities(cols, "cell", shuffle_seed)
+            quals = quals[cols.pop("_row").numpy()]
+        save_npz(os.path.join(HERE, "synth", name + ".npz"), d, cols)
+        mito_names = {g for g, m in zip(d.gene_names, d.gene_is_mito) if m}
+        segs = synth_segments(d, cols, quals)
+        run_ref(GatherCellMetrics, segs, os.path.join(HERE, "synth", name + ".cell.csv"),
+                mitochondrial_gene_ids=mito_names)
+        run_ref(GatherGeneMetrics, segs, os.path.join(HERE, "synth", name + ".gene_run.csv"))
+        # grouped gene semantics = GatherGeneMetrics on records stably sorted by gene id
+        gid = cols["gene"].numpy()
+        order = np.argsort(gid, kind="stable")
+        run_ref(GatherGeneMetrics, [segs[i] for i in order],
+                os.path.join(HERE, "synth", name + ".gene_grouped.csv"))
+        manifest[name] = dict(kw, shuffled_within_cells=shuffle_seed,
+                              n_records=int(cols["cell"].numel()),
+                              mito_genes=sorted(mito_names))
+        print("synthetic set", name, manifest[name]["n_records"], "records")
+
+    with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+        json.dump({"reference": "fredlas/sctools @ /root/reference (2025-02-28 snapshot)",
+                   "bams": BAMS, "synthetic": manifest}, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
