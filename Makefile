@@ -1,0 +1,22 @@
+# Builds the gfx950 HIP engine and the CPU oracle in-tree.
+HIPCC ?= /opt/rocm/bin/hipcc
+HIPFLAGS ?= --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -Wall
+ENGINE := sctools_amd/libsctools_gpu.so
+SRC := sctools_amd/csrc/sct_engine.hip
+HDRS := $(wildcard sctools_amd/csrc/*.h) include/sctools_gpu.h
+
+all: $(ENGINE) oracle/liboracle.so tests/native/libfxcheck.so
+
+$(ENGINE): $(SRC) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC)
+
+oracle/liboracle.so: oracle/sct_oracle.c include/sctools_gpu.h
+	$(MAKE) -s -C oracle liboracle.so
+
+tests/native/libfxcheck.so: tests/native/fxcheck.cpp sctools_amd/csrc/fixedpt.h
+	g++ -O2 -std=c++17 -ffp-contract=off -fPIC -shared -o $@ tests/native/fxcheck.cpp
+
+clean:
+	rm -f $(ENGINE) oracle/liboracle.so tests/native/libfxcheck.so
+
+.PHONY: all clean

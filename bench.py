@@ -1,0 +1,237 @@
+"""
+Benchmark: aligned records/s for cell + gene metrics on MI355X (BASELINE.json).
+
+One step = one pass of the hot path over this rank's synthetic shard, already
+resident in HBM: per-cell metrics (RUN mode over the cell-sorted records) plus
+per-gene metrics (grouped per-gene partials, an RCCL all-reduce across ranks
+when N > 1, finalize), with both sets of entity rows copied back to the host.
+
+Workload: per rank 100M cell-sorted records over
+10k cells (lognormal(0,1) reads per cell), 30k genes (Zipf 1.1, plus None and
+multi-gene ids), 10-mer UMIs; generated on the GPU.  Ranks hold disjoint
+cells (the SplitBam cell-sharding invariant), so N GPUs process N x 100M
+records: weak scaling.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_HBM = 8.0e12  # MI355X HBM3E spec, MI355X_MICROARCH.md
+
+# Algorithmic HBM bytes per record per launch of each kernel.
+ALG_BYTES = {
+    "radix_downsweep": 24,   # read key 8 + value 4, write key 8 + value 4
+    "radix_upsweep": 8,      # read key
+    "reduce_sorted": 44,     # read sorted key 8 + value 4, gather the 32-byte record
+    "build_keys": 33,        # read cell/gene/umi/ref/pos (20) + bits (1), write key 8 + value 4
+    "heads": 4,              # read the entity column
+    "welford": 10,           # read the quality columns
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--records", type=int, default=100_000_000, help="records per rank")
+    ap.add_argument("--cells", type=int, default=10_000, help="cells per rank")
+    ap.add_argument("--genes", type=int, default=30_000)
+    ap.add_argument("--float-mode", default="exact", choices=["exact", "welford"])
+    ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="target seconds of CPU baseline work")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from sctools_amd import engine as E
+    from sctools_amd import synth
+
+    eng = E.get_engine(dev)
+    t0 = time.time()
+    cfg = synth.SynthConfig(n_reads=args.records, n_cells=args.cells, n_genes=args.genes, sigma=1.0,
+                            seed=args.seed + 1000 * rank)
+    data = synth.generate(cfg, device=dev, chunk=16_000_000)
+    torch.cuda.synchronize()
+    if rank == 0:
+        log("generated %d records/rank in %.1fs" % (args.records, time.time() - t0))
+    dims = E.Dims(data.n_cell_ids, data.n_gene_ids, data.n_umi_ids)
+    mito = torch.from_numpy(data.gene_is_mito).to(dev)
+    multi = torch.from_numpy(data.gene_is_multi).to(dev)
+    n_ent = eng.count_entities(data.cols, "cell", dims)
+    partials = torch.empty((data.n_gene_ids, 64), dtype=torch.int64, device=dev)
+    host_cells = torch.empty((n_ent, 24), dtype=torch.int64, pin_memory=True)
+    host_cellf = torch.empty((n_ent, 12), dtype=torch.float64, pin_memory=True)
+    host_genei = torch.empty((data.n_gene_ids, 24), dtype=torch.int64, pin_memory=True)
+    host_genef = torch.empty((data.n_gene_ids, 12), dtype=torch.float64, pin_memory=True)
+
+    def step():
+        ci, cf = eng.compute(data.cols, "cell", dims, mito, multi, float_mode=args.float_mode, n_entities=n_ent)
+        eng.gene_partials(data.cols, dims, out=partials)
+        if world > 1:
+            dist.all_reduce(partials, op=dist.ReduceOp.SUM)
+        gi, gf = eng.finalize_partials(partials)
+        host_cells[: ci.shape[0]].copy_(ci, non_blocking=True)
+        host_cellf[: cf.shape[0]].copy_(cf, non_blocking=True)
+        host_genei.copy_(gi, non_blocking=True)
+        host_genef.copy_(gf, non_blocking=True)
+        return ci.shape[0]
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rows = step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    eng.profile_enable(False)
+    prof = eng.profile_read()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # sanity: every record accounted on both sides
+    n_cell_reads = int(host_cells[:rows, 0].sum())
+    assert n_cell_reads == args.records, (n_cell_reads, args.records)
+    assert int(host_genei[:, 0].sum()) == args.records * world
+
+    total_records = args.records * world * args.steps
+    value = total_records / elapsed
+    # dominant kernel by total time in the timed region (HIP events on the launch stream)
+    dom = max(prof.items(), key=lambda kv: kv[1][0])
+    dom_name, (dom_ms, dom_launches) = dom
+    avg_s = dom_ms / 1e3 / max(1, dom_launches)
+    per_launch_bytes = ALG_BYTES.get(dom_name, 0) * args.records
+    achieved = per_launch_bytes / avg_s if avg_s > 0 else 0.0
+    roofline = {
+        "bound": "hbm",
+        "kernel": dom_name,
+        "achieved": achieved / 1e9,
+        "peak": PEAK_HBM / 1e9,
+        "unit": "GB/s",
+        "frac": achieved / PEAK_HBM,
+        "traffic": None,
+        "avg_launch_ms": avg_s * 1e3,
+        "launches_per_step": dom_launches / args.steps,
+        "alg_bytes_per_record": ALG_BYTES.get(dom_name, 0),
+    }
+    kernel_ms_per_step = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(data, args)
+
+    if rank == 0:
+        out = {
+            "metric": "aligned records/sec for cell+gene metrics",
+            "value": value,
+            "unit": "records/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (SURVEY.md 8(d) config-2 generator, generated on GPU)",
+            "config": {
+                "workload": "config2: %d cell-sorted records/rank, %d cells/rank, %d genes; cell metrics + "
+                            "grouped gene metrics%s" % (args.records, args.cells, args.genes,
+                                                        " + RCCL all-reduce" if world > 1 else ""),
+                "records_per_rank": args.records,
+                "cells_per_rank": args.cells,
+                "genes": args.genes,
+                "float_mode": args.float_mode,
+                "parallelism": "cell-sharded x%d" % world,
+            },
+            "roofline": roofline,
+            "kernel_ms_per_step": kernel_ms_per_step,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(data, args):
+    """Oracle (C restatement, OpenMP over entities) on a bounded leading sample of the shard."""
+    from oracle import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    cols = data.cols
+    cell = cols["cell"]
+
+    def sample(n):
+        n = min(n, cell.numel())
+        # cut at a cell boundary so every cell in the sample is complete
+        c_last = int(cell[n - 1].item())
+        n = int(torch.searchsorted(cell, torch.tensor([c_last], dtype=cell.dtype, device=cell.device),
+                                   right=False).item()) or n
+        h = {c: t[:n].cpu().numpy() for c, t in cols.items()}
+        for c in ("gq_sum", "gq_len", "gq_gt30"):
+            h[c] = h[c].view(np.uint16)
+        return n, h
+
+    def run(h):
+        t0 = time.perf_counter()
+        O.run(h, "cell", data.gene_is_mito, data.n_gene_ids, threads=threads)
+        O.run(h, "gene_grouped", data.gene_is_mito, data.n_gene_ids, threads=threads)
+        return time.perf_counter() - t0
+
+    n0, h0 = sample(2_000_000)
+    t_probe = run(h0)
+    rate = n0 / max(t_probe, 1e-6)
+    n1, h1 = sample(int(min(cell.numel(), rate * args.cpu_sample_s)))
+    t1 = run(h1)
+    return {
+        "value": n1 / t1,
+        "unit": "records/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": "first %d records (%d whole cells) of rank 0's shard: oracle cell metrics + grouped gene "
+                  "metrics, %.1fs" % (n1, int(h1["cell"][-1]) + 1, t1),
+    }
+
+
+if __name__ == "__main__":
+    main()

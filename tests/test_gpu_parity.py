@@ -1,0 +1,169 @@
+"""HIP engine parity: the GPU path against the reference's outputs and the oracle.
+
+* bundled BAMs and synthetic fixture sets: SCT_FLOAT_WELFORD output must be
+  byte-identical to the reference CSVs; SCT_FLOAT_EXACT_SUM must match every
+  integer and every float within 1e-9 relative (north-star tolerance);
+* larger synthetic sets generated on the GPU: ints identical to the oracle,
+  Welford floats bit-identical, exact-sum floats within 1e-9;
+* size-independent properties at multi-million records.
+"""
+import numpy as np
+import pytest
+import torch
+
+import helpers as H
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from sctools_amd import engine as E
+
+    return E.get_engine("cuda:0")
+
+
+def dims_of(n_cells, n_genes, n_umis):
+    from sctools_amd import engine as E
+
+    return E.Dims(n_cells, n_genes, n_umis)
+
+
+def run_gpu(eng, arrays, mode, dims, mito, float_mode):
+    from sctools_amd import engine as E
+
+    cols = E.to_device(arrays, eng.device)
+    gm = torch.from_numpy(np.ascontiguousarray(mito, dtype=np.uint8)).to(eng.device)
+    if mode == "gene_grouped":
+        part = eng.gene_partials(cols, dims)
+        gi, gf = eng.finalize_partials(part)
+    else:
+        gi, gf = eng.compute(cols, mode, dims, gm, gm, float_mode=float_mode)
+    return gi.cpu().numpy(), gf.cpu().numpy()
+
+
+@pytest.mark.parametrize("bam", H.BAMS)
+@pytest.mark.parametrize("mode", ["cell", "gene"])
+def test_bundled_bams_welford_byte_identical(eng, bam, mode):
+    cols = H.bam_columns(bam, mode)
+    mito, _ = cols.gene_flags()
+    d = dims_of(len(cols.cells), len(cols.genes), len(cols.umis))
+    gi, gf = run_gpu(eng, cols.arrays, mode, d, mito, "welford")
+    got = H.render(mode, gi, gf, cols.arrays, cols.cells.names, cols.genes.names)
+    assert got == H.golden_text(bam, mode)
+
+
+@pytest.mark.parametrize("bam", H.BAMS)
+@pytest.mark.parametrize("mode", ["cell", "gene"])
+def test_bundled_bams_exact_sum_within_tolerance(eng, bam, mode):
+    cols = H.bam_columns(bam, mode)
+    mito, _ = cols.gene_flags()
+    d = dims_of(len(cols.cells), len(cols.genes), len(cols.umis))
+    gi, gf = run_gpu(eng, cols.arrays, mode, d, mito, "exact")
+    got = H.render(mode, gi, gf, cols.arrays, cols.cells.names, cols.genes.names)
+    H.assert_csv_close(got, H.golden_text(bam, mode), rel=REL)
+
+
+@pytest.mark.parametrize("name", H.SYNTH)
+@pytest.mark.parametrize("mode,kind", [("cell", "cell"), ("gene", "gene_run")])
+@pytest.mark.parametrize("float_mode", ["welford", "exact"])
+def test_synthetic_fixtures(eng, name, mode, kind, float_mode):
+    s = H.synth(name)
+    gi, gf = run_gpu(eng, s.arrays, mode, dims_of(*s.dims), s.gene_is_mito, float_mode)
+    got = H.render(mode, gi, gf, s.arrays, s.cell_names, s.gene_names)
+    if float_mode == "welford":
+        assert got == H.synth_text(name, kind)
+    else:
+        H.assert_csv_close(got, H.synth_text(name, kind), rel=REL)
+
+
+@pytest.mark.parametrize("name", H.SYNTH)
+def test_synthetic_grouped_gene(eng, name):
+    s = H.synth(name)
+    gi, gf = run_gpu(eng, s.arrays, "gene_grouped", dims_of(*s.dims), s.gene_is_mito, "exact")
+    got = H.render("gene_grouped", gi, gf, s.arrays, s.cell_names, s.gene_names)
+    H.assert_csv_close(got, H.synth_text(name, "gene_grouped"), rel=REL)
+
+
+def gpu_synth(n, cells, genes, seed, sigma=1.0, **kw):
+    from sctools_amd import synth
+
+    return synth.generate(synth.SynthConfig(n_reads=n, n_cells=cells, n_genes=genes, seed=seed, sigma=sigma,
+                                            **kw), device="cuda:0")
+
+
+def host_cols(d):
+    h = {c: t.cpu().numpy() for c, t in d.cols.items()}
+    for c in ("gq_sum", "gq_len", "gq_gt30"):
+        h[c] = h[c].view(np.uint16)
+    return h
+
+
+def compare(gi, gf, oi, of, exact_floats):
+    assert gi.shape == oi.shape
+    assert np.array_equal(gi, oi)
+    nan_g, nan_o = np.isnan(gf), np.isnan(of)
+    assert np.array_equal(nan_g, nan_o)
+    if exact_floats:
+        assert np.array_equal(gf[~nan_g], of[~nan_o])
+    else:
+        a, b = gf[~nan_g], of[~nan_o]
+        rel = np.abs(a - b) / np.maximum(np.maximum(np.abs(a), np.abs(b)), 1e-300)
+        assert (rel <= REL).all(), rel.max()
+
+
+@pytest.mark.parametrize("seed,n,cells,genes,sigma", [
+    (21, 300_000, 60, 3_000, 1.0),
+    (22, 2_000_000, 200, 30_000, 1.0),
+    (23, 1_500_000, 2_000, 5_000, 2.0),
+])
+def test_gpu_generated_against_oracle(eng, seed, n, cells, genes, sigma):
+    from sctools_amd import engine as E
+
+    d = gpu_synth(n, cells, genes, seed, sigma=sigma, p_none_cell_reads=0.005)
+    h = host_cols(d)
+    dims = E.Dims(d.n_cell_ids, d.n_gene_ids, d.n_umi_ids)
+    mito = torch.from_numpy(d.gene_is_mito).to(eng.device)
+    for mode in ("cell", "gene"):
+        oi, of = O.run(h, mode, d.gene_is_mito, d.n_gene_ids, threads=8)
+        for fm in ("welford", "exact"):
+            gi, gf = eng.compute(d.cols, mode, dims, mito, mito, float_mode=fm)
+            compare(gi.cpu().numpy(), gf.cpu().numpy(), oi, of, exact_floats=(fm == "welford"))
+    oi, of = O.run(h, "gene_grouped", d.gene_is_mito, d.n_gene_ids, threads=8)
+    gi, gf = eng.finalize_partials(eng.gene_partials(d.cols, dims))
+    gi, gf = gi.cpu().numpy(), gf.cpu().numpy()
+    live = oi[:, 0] > 0
+    assert np.array_equal(gi[:, 0] > 0, live)
+    compare(gi[live], gf[live], oi[live], of[live], exact_floats=False)
+
+
+def test_properties_at_scale(eng):
+    """Size-independent invariants on 20M records (the oracle would take too long)."""
+    from sctools_amd import engine as E
+    from sctools_amd import _native as N
+
+    d = gpu_synth(20_000_000, 2_000, 30_000, 31)
+    dims = E.Dims(d.n_cell_ids, d.n_gene_ids, d.n_umi_ids)
+    mito = torch.from_numpy(d.gene_is_mito).to(eng.device)
+    ci, cf = eng.compute(d.cols, "cell", dims, mito, mito, float_mode="exact")
+    ci2, cf2 = eng.compute(d.cols, "cell", dims, mito, mito, float_mode="exact")
+    assert torch.equal(ci, ci2) and torch.equal(torch.nan_to_num(cf, 7.0), torch.nan_to_num(cf2, 7.0))
+    gi, gf = eng.finalize_partials(eng.gene_partials(d.cols, dims))
+    n = d.cols["cell"].numel()
+    assert int(ci[:, N.I_N_READS].sum()) == n
+    assert int(gi[:, N.I_N_READS].sum()) == n
+    # every molecule / fragment is counted once from the cell side and once from the gene side
+    for col in (N.I_N_MOL, N.I_N_FRAG, N.I_MOL_SINGLE, N.I_FRAG_SINGLE, N.I_DUP, N.I_SPLICED):
+        assert int(ci[:, col].sum()) == int(gi[:, col].sum())
+    # (cell, gene) pairs: sum of n_genes over cells == sum of cells_expressing over genes
+    assert int(ci[:, N.I_N_K1].sum()) == int(gi[:, N.I_N_K1].sum())
+    assert int(ci[:, N.I_K1_MULTI].sum()) == int(gi[:, N.I_K1_MULTI].sum())
+    # Welford and exact-sum agree within tolerance at this size
+    wi, wf = eng.compute(d.cols, "cell", dims, mito, mito, float_mode="welford")
+    assert torch.equal(wi, ci)
+    a, b = wf.cpu().numpy(), cf.cpu().numpy()
+    ok = np.isclose(a, b, rtol=REL, atol=0) | (np.isnan(a) & np.isnan(b))
+    assert ok.all()
