@@ -35,8 +35,9 @@ PEAK_HBM = 8.0e12  # MI355X HBM3E spec, MI355X_MICROARCH.md
 ALG_BYTES = {
     "radix_downsweep": 24,   # read key 8 + value 4, write key 8 + value 4
     "radix_upsweep": 8,      # read key
-    "reduce_sorted": 44,     # read sorted key 8 + value 4, gather the 32-byte record
+    "reduce_sorted": 60,     # read sorted key 8 + value 4, gather the 32-byte record, write 16-byte gene payload
     "build_keys": 33,        # read cell/gene/umi/ref/pos (20) + bits (1), write key 8 + value 4
+    "gene_reduce": 16,       # read the 16-byte gene contribution
     "heads": 4,              # read the entity column
     "welford": 10,           # read the quality columns
 }
@@ -96,8 +97,12 @@ def main():
     host_genef = torch.empty((data.n_gene_ids, 12), dtype=torch.float64, pin_memory=True)
 
     def step():
-        ci, cf = eng.compute(data.cols, "cell", dims, mito, multi, float_mode=args.float_mode, n_entities=n_ent)
-        eng.gene_partials(data.cols, dims, out=partials)
+        if args.float_mode == "exact":
+            # one pass: cell rows + grouped gene partials share the cell-view sort
+            ci, cf, _ = eng.cell_and_gene(data.cols, dims, mito, n_entities=n_ent, partials=partials)
+        else:
+            ci, cf = eng.compute(data.cols, "cell", dims, mito, multi, float_mode=args.float_mode, n_entities=n_ent)
+            eng.gene_partials(data.cols, dims, out=partials)
         if world > 1:
             dist.all_reduce(partials, op=dist.ReduceOp.SUM)
         gi, gf = eng.finalize_partials(partials)

@@ -98,8 +98,12 @@ typedef struct sct_plan {
   int32_t n_cell_ids;   /* dictionary sizes: ids are in [0, n_*_ids)      */
   int32_t n_gene_ids;
   int32_t n_umi_ids;
-  int32_t reserved;
+  int32_t flags;        /* SCT_PLAN_* bits                                */
 } sct_plan_t;
+
+/* plan.flags: size the workspace for grouped gene partials next to cell rows
+ * (sct_cell_metrics_gene_partials).  Implied by SCT_MODE_GENE_GROUPED. */
+#define SCT_PLAN_GENE_PARTIALS 0x1
 
 /* ---- output rows ----
  * ints [rows][SCT_NI] (int64) and floats [rows][SCT_NF] (double).  Column
@@ -187,10 +191,22 @@ int sct_compute_metrics(const sct_plan_t* plan, const sct_records_t* rec,
 
 /* Per-gene additive partials (GROUPED mode) of this rank's records, written
  * to `partials` [n_gene_ids][SCT_NP] (overwritten).  Records must be
- * cell-sharded (no cell run split across calls), the SplitBam invariant
- * (bam.py:439-448). */
+ * cell-sorted with every cell id in one run (SCT_EINVAL otherwise) and
+ * cell-sharded across calls: the SplitBam invariant (bam.py:439-448).  The
+ * (gene, cell, umi) Counters of the gene view are resolved in the cell-sorted
+ * order, so this runs the cell pipeline internally.  Synchronizes `stream`. */
 int sct_gene_partials(const sct_plan_t* plan, const sct_records_t* rec, void* workspace,
                       size_t workspace_bytes, int64_t* partials, void* stream);
+
+/* Cell rows (as sct_compute_metrics with SCT_MODE_CELL) AND grouped gene
+ * partials (as sct_gene_partials) from one pass over cell-sorted records:
+ * GatherCellMetrics + GatherGeneMetrics of the same shard sharing one sort.
+ * `plan->mode` must be SCT_MODE_CELL with SCT_PLAN_GENE_PARTIALS in flags. */
+int sct_cell_metrics_gene_partials(const sct_plan_t* plan, const sct_records_t* rec,
+                                   const uint8_t* gene_is_mito, void* workspace,
+                                   size_t workspace_bytes, int64_t* out_ints, double* out_floats,
+                                   int64_t capacity, int64_t* n_rows /* host */,
+                                   int64_t* gene_partials, void* stream);
 
 /* Finalize `rows` partial rows into output rows (floats and ratios; the
  * reference's finalize(), aggregator.py:342-387, 463-490, 571-578).  `mode`

@@ -33,8 +33,9 @@ RECORD_COLUMNS = ("cell", "umi", "gene", "ref", "pos", "gq_sum", "gq_len", "gq_g
                   "cy_gt30", "cy_len", "uy_gt30", "uy_len")
 
 EXPORTED = ("sct_abi_version", "sct_last_error", "sct_workspace_size", "sct_count_entities",
-            "sct_compute_metrics", "sct_gene_partials", "sct_finalize_partials",
-            "sct_profile_enable", "sct_profile_read")
+            "sct_compute_metrics", "sct_gene_partials", "sct_cell_metrics_gene_partials",
+            "sct_finalize_partials", "sct_profile_enable", "sct_profile_read")
+PLAN_GENE_PARTIALS = 0x1
 
 
 class Records(ctypes.Structure):
@@ -50,7 +51,7 @@ class Plan(ctypes.Structure):
         ("n_cell_ids", ctypes.c_int32),
         ("n_gene_ids", ctypes.c_int32),
         ("n_umi_ids", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
     ]
 
 
@@ -87,6 +88,9 @@ def load() -> ctypes.CDLL:
                                       ctypes.c_size_t, vp, vp, i64, ctypes.POINTER(i64), vp]
     L.sct_gene_partials.restype = ctypes.c_int
     L.sct_gene_partials.argtypes = [ctypes.POINTER(Plan), ctypes.POINTER(Records), vp, ctypes.c_size_t, vp, vp]
+    L.sct_cell_metrics_gene_partials.restype = ctypes.c_int
+    L.sct_cell_metrics_gene_partials.argtypes = [ctypes.POINTER(Plan), ctypes.POINTER(Records), vp, vp,
+                                                 ctypes.c_size_t, vp, vp, i64, ctypes.POINTER(i64), vp, vp]
     L.sct_finalize_partials.restype = ctypes.c_int
     L.sct_finalize_partials.argtypes = [i32, vp, i64, vp, vp, vp]
     L.sct_profile_enable.restype = ctypes.c_int

@@ -38,9 +38,49 @@ constexpr int P_FLOAT = SCT_P_FLOAT_BASE;  // 24: stream s lanes at P_FLOAT + 8*
 constexpr int kStreams = 4;                // UY frac, genomic frac, genomic mean quality, CY frac
 static_assert(SCT_P_FLOAT_BASE + kStreams * 8 <= SCT_NP, "partials row too small");
 
+constexpr uint32_t kUnmappedValBit = 0x80000000u;  // sort value bit 31: the record is unmapped
+
 struct Bits {  // key layout: [entity | k1 | k2 | hash]
   int e, k1, k2, h;
   int total() const { return e + k1 + k2 + h; }
 };
+
+}  // namespace sct
+
+namespace sct {
+
+// ---- gene view: one 16-byte contribution per record, emitted by the cell-view pass ----
+// Everything GatherGeneMetrics derives per record, with the distinct-count events of the
+// (gene, cell, umi) Counters already resolved in the cell-sorted order (molecules,
+// fragments and (cell, gene) pairs are the same sets in both views).
+enum : uint32_t {
+  GF_PERFECT_UMI = 1u << 0,
+  GF_EXONIC = 1u << 1,
+  GF_INTRONIC = 1u << 2,
+  GF_UTR = 1u << 3,
+  GF_UNIQUE = 1u << 4,
+  GF_MULTIPLE = 1u << 5,
+  GF_DUP = 1u << 6,
+  GF_SPLICED = 1u << 7,
+  GF_MOL_HEAD = 1u << 8,
+  GF_MOL_SINGLE = 1u << 9,
+  GF_FRAG_FIRST = 1u << 10,
+  GF_FRAG_SINGLE = 1u << 11,
+  GF_CG_HEAD = 1u << 12,   // first record of a (cell, gene) pair -> number_cells_expressing
+  GF_CG_MULTI = 1u << 13,  // ... of a pair with > 1 record -> number_cells_detected_multiple
+};
+constexpr int kGeneFlags = 14;
+
+struct __attribute__((aligned(16))) GenePayload {
+  uint32_t gene;
+  uint16_t flags;
+  uint8_t uy_gt30, uy_len;
+  uint16_t gq_gt30, gq_len, gq_sum, pad;
+};
+static_assert(sizeof(GenePayload) == 16, "gene payload must be 16 bytes");
+
+constexpr int kGenesPerBucket = 128;  // LDS bins of one gene bucket
+constexpr int kMaxGeneBuckets = 2048;
+constexpr int kGeneLanes = 1 + kGeneFlags + 3 * 8;  // n_reads, 14 flag counts, 3 streams x 8 lanes
 
 }  // namespace sct

@@ -1,0 +1,76 @@
+// scan.h -- device-wide exclusive scans (reduce / small scan / apply).
+#pragma once
+#include "util.h"
+
+namespace sct {
+
+constexpr int kScanChunk = 4096;
+
+__global__ void k_scan_reduce(const uint32_t* __restrict__ in, int64_t m, uint64_t* __restrict__ sums) {
+  const int64_t base = (int64_t)blockIdx.x * kScanChunk;
+  uint64_t s = 0;
+  for (int i = threadIdx.x; i < kScanChunk; i += kBlock) {
+    const int64_t p = base + i;
+    if (p < m) s += in[p];
+  }
+  __shared__ uint64_t red[kWaves];
+  s = wave_sum(s);
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < kWaves; w++) t += red[w];
+    sums[blockIdx.x] = t;
+  }
+}
+
+// one block: exclusive scan of m uint64 in place; the total goes to *out_total (if set)
+__global__ void k_scan_small(uint64_t* __restrict__ data, int64_t m, uint64_t* __restrict__ out_total) {
+  __shared__ uint64_t lds[kWaves + 1];
+  uint64_t carry = 0;
+  for (int64_t base = 0; base < m; base += kBlock) {
+    const int64_t p = base + threadIdx.x;
+    const uint64_t v = p < m ? data[p] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_exclusive_scan<uint64_t>(v, &tot, lds);
+    if (p < m) data[p] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0 && out_total) *out_total = carry;
+}
+
+__global__ void k_scan_apply(const uint32_t* __restrict__ in, int64_t m, const uint64_t* __restrict__ block_off,
+                             uint32_t* __restrict__ out) {
+  __shared__ uint64_t lds[kWaves + 1];
+  const int64_t base = (int64_t)blockIdx.x * kScanChunk;
+  const uint64_t carry = block_off[blockIdx.x];
+  constexpr int per = kScanChunk / kBlock;
+  uint32_t v[per];
+  uint64_t s = 0;
+  const int64_t p0 = base + (int64_t)threadIdx.x * per;
+#pragma unroll
+  for (int j = 0; j < per; j++) {
+    const int64_t p = p0 + j;
+    v[j] = p < m ? in[p] : 0;
+    s += v[j];
+  }
+  uint64_t tot;
+  uint64_t ex = block_exclusive_scan<uint64_t>(s, &tot, lds) + carry;
+#pragma unroll
+  for (int j = 0; j < per; j++) {
+    const int64_t p = p0 + j;
+    if (p < m) out[p] = (uint32_t)ex;
+    ex += v[j];
+  }
+}
+
+// exclusive scan of m uint32 counts into `out`; `sums` needs cdiv(m, kScanChunk) entries
+inline int scan_counts(const uint32_t* in, int64_t m, uint32_t* out, uint64_t* sums, hipStream_t s) {
+  const int64_t chunks = cdiv(m, kScanChunk);
+  LAUNCH("scan", k_scan_reduce, dim3((unsigned)chunks), dim3(kBlock), s, in, m, sums);
+  LAUNCH("scan", k_scan_small, dim3(1), dim3(kBlock), s, sums, chunks, (uint64_t*)nullptr);
+  LAUNCH("scan", k_scan_apply, dim3((unsigned)chunks), dim3(kBlock), s, in, m, (const uint64_t*)sums, out);
+  return SCT_OK;
+}
+
+}  // namespace sct

@@ -1,0 +1,277 @@
+// segment.h -- the input-order pass: entity runs (bam.iter_tag_groups, bam.py:492-540),
+// packed sort keys, and every per-record additive metric of the entity.
+//
+// One block owns a tile of kTile consecutive records.  The entity column is staged
+// into LDS with coalesced loads, run heads are found on blocked items, and a block
+// scan numbers the runs.  Then each thread walks the tile in striped order (all
+// column loads coalesced), builds the key [run | k1 | k2 | fragment hash] and the
+// value (record index, bit 31 = unmapped), and sums the metrics that are plain
+// per-record sums in the reference (aggregator.py:259-334, 507-530) into the run's
+// partial row: n_reads, barcode / alignment counters, and the exact fixed-point
+// lanes of the quality streams (fixedpt.h).  Runs are contiguous in input order, so
+// a thread flushes once per run it touches and a wave once per tile.
+#pragma once
+#include "fixedpt.h"
+#include "radix.h"
+#include "reduce.h"
+#include "util.h"
+
+namespace sct {
+
+// heads per tile.  With `seen` set (grouped gene partials), every run head also bumps
+// seen[entity value]; a value seen twice means the column is not sorted into single
+// runs and *dup_flag is raised.
+__global__ void k_heads(const int32_t* __restrict__ key, int64_t n, uint64_t* __restrict__ tile_cnt,
+                        uint32_t* __restrict__ seen, uint64_t* __restrict__ dup_flag) {
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  uint64_t c = 0;
+#pragma unroll 4
+  for (int j = 0; j < kItems; j++) {
+    const int64_t p = base + (int64_t)j * kBlock + threadIdx.x;
+    if (p < n) {
+      const int32_t v = key[p];
+      const bool h = (p == 0 || v != key[p - 1]);
+      c += h ? 1 : 0;
+      if (h && seen) {
+        if (atomicAdd(&seen[v], 1u) != 0u) atomicOr((unsigned long long*)dup_flag, 1ull);
+      }
+    }
+  }
+  __shared__ uint64_t red[kWaves];
+  c = wave_sum(c);
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < kWaves; w++) t += red[w];
+    tile_cnt[blockIdx.x] = t;
+  }
+}
+
+struct KeyCols {
+  const int32_t* ent;  // column whose runs are the entities
+  const int32_t* k1;
+  const int32_t* k2;
+};
+
+__device__ __forceinline__ uint64_t make_key(uint64_t e, uint32_t k1, uint32_t k2, uint32_t hash, const Bits& b) {
+  const uint64_t hv = b.h ? (uint64_t)(hash >> (32 - b.h)) : 0;  // top bits of the fragment mix
+  return (e << (b.k1 + b.k2 + b.h)) | ((uint64_t)k1 << (b.k2 + b.h)) | ((uint64_t)k2 << b.h) | hv;
+}
+
+// per-record additive counters of one run
+template <bool kCell>
+struct AddAcc {
+  static constexpr int kK = kCell ? 13 : 9;
+  int64_t v[kK];
+  // counter i -> partial slot: 0..8 are P_N_READS..P_SPLICED; 9..12 are P_PERFECT_CB, P_INTERGENIC,
+  // P_UNMAPPED, P_MITO_READS
+  static __device__ __forceinline__ int slot(int i) {
+    return i < 9 ? i : (i < 12 ? P_PERFECT_CB + (i - 9) : P_MITO_READS);
+  }
+  __device__ __forceinline__ void clear() {
+#pragma unroll
+    for (int i = 0; i < kK; i++) v[i] = 0;
+  }
+};
+
+// Stage the tile's entity column, find run heads, and number the runs: s_e[q] = run index of
+// tile position q.  Writes ent_start[run] for heads when ent_start is set.  Block-wide (barriers).
+__device__ __forceinline__ void tile_run_ids(const int32_t* __restrict__ ent, int64_t n, int64_t base, int tile_n,
+                                             uint64_t tile_off, int32_t* s_e, int32_t* s_prev, uint64_t* s_scan,
+                                             int64_t* __restrict__ ent_start) {
+  const int t = threadIdx.x;
+#pragma unroll 4
+  for (int j = 0; j < kItems; j++) {
+    const int q = j * kBlock + t;
+    if (q < tile_n) s_e[q] = ent[base + q];
+  }
+  if (t == 0) *s_prev = base > 0 ? ent[base - 1] : 0;
+  __syncthreads();
+  const int q0 = t * kItems;
+  uint32_t heads = 0;
+  {
+    int32_t prev = q0 > 0 ? s_e[q0 - 1] : *s_prev;
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      const int q = q0 + j;
+      if (q < tile_n) {
+        const int32_t v = s_e[q];
+        const bool h = (base + q == 0) || v != prev;
+        heads |= (h ? 1u : 0u) << j;
+        prev = v;
+      }
+    }
+  }
+  uint64_t tot;
+  const uint64_t ex = block_exclusive_scan<uint64_t>((uint64_t)__popc(heads), &tot, s_scan);  // has barriers
+  int64_t e = (int64_t)(tile_off + ex) - 1;
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    const int q = q0 + j;
+    if (q >= tile_n) break;
+    if (heads & (1u << j)) {
+      e += 1;
+      if (ent_start) ent_start[e] = base + q;
+    }
+    s_e[q] = (int32_t)e;
+  }
+  __syncthreads();
+}
+
+template <bool kCell, bool kGene>
+__global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r, const uint8_t* __restrict__ k1_is_mito,
+                                                           int64_t n, const uint64_t* __restrict__ tile_off, Bits b,
+                                                           uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                           int64_t* __restrict__ ent_start,
+                                                           int64_t* __restrict__ partials,
+                                                           uint32_t* __restrict__ gene_counts, int n_buckets) {
+  static_assert(!kGene || kCell, "gene buckets come from the cell view");
+  __shared__ int32_t s_e[kTile];
+  __shared__ int32_t s_prev;
+  __shared__ uint64_t s_scan[kWaves + 1];
+  __shared__ uint32_t s_hist[kGene ? kMaxGeneBuckets : 1];
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
+  if (kGene)
+    for (int i = t; i < n_buckets; i += kBlock) s_hist[i] = 0;
+  // 1-2. run index of every record of the tile
+  tile_run_ids(c.ent, n, base, tile_n, tile_off[blockIdx.x], s_e, &s_prev, s_scan, ent_start);
+
+  // 3. striped pass: keys, values and the run's additive metrics.  Runs are contiguous, so
+  // in a round the wave's lanes cross a run boundary together: flush wave-cooperatively.
+  using A = AddAcc<kCell>;
+  A acc;
+  acc.clear();
+  int64_t cur_e = -1;
+  const auto slot = [](int i) { return A::slot(i); };
+  for (int j = 0; j < kItems; j++) {
+    const int q = j * kBlock + t;
+    const bool valid = q < tile_n;
+    const int64_t p = base + q;
+    const int64_t e = valid ? (int64_t)s_e[q] : cur_e;
+    wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
+    if (!valid) continue;
+    cur_e = e;
+    const uint32_t k1 = (uint32_t)c.k1[p];
+    const uint32_t k2 = (uint32_t)c.k2[p];
+    const uint8_t bt = r.bits[p];
+    const uint8_t xf = r.xf[p];
+    const bool mapped = !(bt & SCT_B_UNMAPPED);
+    const uint32_t hsh = mapped ? frag_hash(r.ref[p], r.pos[p], (bt & SCT_B_REVERSE) ? 1u : 0u) : 0u;
+    keys[p] = make_key((uint64_t)e, k1, k2, hsh, b);
+    vals[p] = (uint32_t)p | (mapped ? 0u : kUnmappedValBit);
+    // MetricAggregator.parse_molecule (aggregator.py:259-334)
+    acc.v[0] += 1;
+    acc.v[1] += (bt & SCT_B_PERFECT_UMI) ? 1 : 0;
+    if (mapped) {
+      const bool nh1 = bt & SCT_B_NH1;
+      acc.v[2] += (xf == SCT_XF_CODING);
+      acc.v[3] += (xf == SCT_XF_INTRONIC);
+      acc.v[4] += (xf == SCT_XF_UTR);
+      acc.v[5] += nh1 ? 1 : 0;
+      acc.v[6] += nh1 ? 0 : 1;
+      acc.v[7] += (bt & SCT_B_DUPLICATE) ? 1 : 0;
+      acc.v[8] += (bt & SCT_B_SPLICED) ? 1 : 0;
+    }
+    if constexpr (kCell) {
+      // CellMetrics.parse_extra_fields (aggregator.py:507-530) + mito reads (463-490)
+      acc.v[9] += ((bt & SCT_B_HAS_CB) && (bt & SCT_B_PERFECT_CB)) ? 1 : 0;
+      acc.v[10] += (xf == SCT_XF_INTERGENIC);
+      acc.v[11] += (xf == SCT_XF_ABSENT);
+      acc.v[12] += k1_is_mito[k1];
+    }
+    if (kGene) atomicAdd(&s_hist[k1 / kGenesPerBucket], 1u);
+  }
+  wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
+  if (kGene) {
+    __syncthreads();
+    const int64_t tiles = gridDim.x;
+    for (int i = t; i < n_buckets; i += kBlock) gene_counts[(int64_t)i * tiles + blockIdx.x] = s_hist[i];
+  }
+}
+
+// Exact fixed-point lanes of the quality streams (fixedpt.h), one run at a time, in input
+// order: UY fraction, genomic fraction, genomic mean quality (aggregator.py:266-292) and,
+// for cells, the CY fraction (aggregator.py:507-514).  Blocked items with 16-byte vector
+// loads; the streams are summed one after another so only 8 lanes are live per thread.
+template <bool kCell>
+__global__ void __launch_bounds__(kBlock) k_stream_sums(const int32_t* __restrict__ ent, RecCols r, int64_t n,
+                                                        const uint64_t* __restrict__ tile_off,
+                                                        int64_t* __restrict__ partials) {
+  __shared__ int32_t s_e[kTile];
+  __shared__ int32_t s_prev;
+  __shared__ uint64_t s_scan[kWaves + 1];
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
+  tile_run_ids(ent, n, base, tile_n, tile_off[blockIdx.x], s_e, &s_prev, s_scan, nullptr);
+
+  const int q0 = t * kItems;
+  const int64_t p0 = base + q0;
+  const bool full = q0 + kItems <= tile_n;
+  constexpr int ns = kCell ? 4 : 3;
+#pragma unroll 1
+  for (int st = 0; st < ns; st++) {
+    // numerator / denominator columns of stream st, kItems consecutive records, packed
+    const void* num = st == 0 ? (const void*)r.uy_gt30 : st == 1 ? (const void*)r.gq_gt30
+                    : st == 2 ? (const void*)r.gq_sum : (const void*)r.cy_gt30;
+    const void* den = st == 0 ? (const void*)r.uy_len : (st == 1 || st == 2) ? (const void*)r.gq_len
+                    : (const void*)r.cy_len;
+    const bool wide = (st == 1 || st == 2);  // uint16 columns
+    uint32_t wn[8], wd[8];
+    if (full) {
+      if (wide) {
+        const uint4 a0 = reinterpret_cast<const uint4*>((const uint16_t*)num + p0)[0];
+        const uint4 a1 = reinterpret_cast<const uint4*>((const uint16_t*)num + p0)[1];
+        const uint4 b0 = reinterpret_cast<const uint4*>((const uint16_t*)den + p0)[0];
+        const uint4 b1 = reinterpret_cast<const uint4*>((const uint16_t*)den + p0)[1];
+        wn[0] = a0.x, wn[1] = a0.y, wn[2] = a0.z, wn[3] = a0.w, wn[4] = a1.x, wn[5] = a1.y, wn[6] = a1.z, wn[7] = a1.w;
+        wd[0] = b0.x, wd[1] = b0.y, wd[2] = b0.z, wd[3] = b0.w, wd[4] = b1.x, wd[5] = b1.y, wd[6] = b1.z, wd[7] = b1.w;
+      } else {
+        const uint4 a0 = *reinterpret_cast<const uint4*>((const uint8_t*)num + p0);
+        const uint4 b0 = *reinterpret_cast<const uint4*>((const uint8_t*)den + p0);
+        wn[0] = a0.x, wn[1] = a0.y, wn[2] = a0.z, wn[3] = a0.w, wn[4] = wn[5] = wn[6] = wn[7] = 0;
+        wd[0] = b0.x, wd[1] = b0.y, wd[2] = b0.z, wd[3] = b0.w, wd[4] = wd[5] = wd[6] = wd[7] = 0;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) wn[k] = wd[k] = 0;
+#pragma unroll
+      for (int j = 0; j < kItems; j++) {
+        const bool ok = q0 + j < tile_n;
+        const uint32_t a = !ok ? 0u : wide ? ((const uint16_t*)num)[p0 + j] : ((const uint8_t*)num)[p0 + j];
+        const uint32_t d = !ok ? 0u : wide ? ((const uint16_t*)den)[p0 + j] : ((const uint8_t*)den)[p0 + j];
+        if (wide) {
+          wn[j / 2] |= a << (16 * (j % 2));
+          wd[j / 2] |= d << (16 * (j % 2));
+        } else {
+          wn[j / 4] |= a << (8 * (j % 4));
+          wd[j / 4] |= d << (8 * (j % 4));
+        }
+      }
+    }
+    int64_t lanes[kStreamLanes];
+#pragma unroll
+    for (int i = 0; i < kStreamLanes; i++) lanes[i] = 0;
+    int64_t cur_e = -1;
+    const int slot0 = P_FLOAT + st * kStreamLanes;
+    const auto slot = [slot0](int i) { return slot0 + i; };
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      const int q = q0 + j;
+      const bool valid = q < tile_n;
+      const int64_t e = valid ? (int64_t)s_e[q] : cur_e;
+      wave_flush<kStreamLanes>(lanes, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
+      if (!valid) continue;
+      cur_e = e;
+      const uint32_t a = wide ? (wn[j / 2] >> (16 * (j % 2))) & 0xffffu : (wn[j / 4] >> (8 * (j % 4))) & 0xffu;
+      const uint32_t d = wide ? (wd[j / 2] >> (16 * (j % 2))) & 0xffffu : (wd[j / 4] >> (8 * (j % 4))) & 0xffu;
+      fx_accumulate(lanes, ratio(a, d));
+    }
+    wave_flush<kStreamLanes>(lanes, cur_e >= 0, cur_e, partials, slot);
+  }
+}
+
+}  // namespace sct

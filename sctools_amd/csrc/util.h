@@ -1,0 +1,184 @@
+// util.h -- host error/profiling plumbing and device helpers shared by the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "common.h"
+
+namespace sct {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / kWave;
+
+// ---------------- host: thread-local error string ----------------
+inline std::string& last_error() {
+  static thread_local std::string e;
+  return e;
+}
+
+inline int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+inline int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  last_error() = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                           \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return ::sct::fail(SCT_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                         __LINE__);                                                            \
+  } while (0)
+
+#define LAUNCHCHK() HIPCHK(hipGetLastError())
+
+// ---------------- host: optional per-kernel timing with HIP events ----------------
+struct ProfEntry {
+  std::string name;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+};
+inline bool& prof_on() {
+  static thread_local bool on = false;
+  return on;
+}
+inline std::vector<ProfEntry>& prof_entries() {
+  static thread_local std::vector<ProfEntry> v;
+  return v;
+}
+
+struct ProfScope {
+  hipEvent_t a = nullptr, b = nullptr;
+  hipStream_t s;
+  const char* name;
+  ProfScope(const char* n, hipStream_t st) : s(st), name(n) {
+    if (prof_on() && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess) (void)hipEventRecord(a, s);
+  }
+  ~ProfScope() {
+    if (!prof_on() || !a || !b) return;
+    (void)hipEventRecord(b, s);
+    for (auto& e : prof_entries())
+      if (e.name == name) {
+        e.ev.emplace_back(a, b);
+        return;
+      }
+    prof_entries().push_back(ProfEntry{name, {{a, b}}});
+  }
+};
+
+#define LAUNCH(name, kern, grid, block, strm, ...)               \
+  do {                                                           \
+    ::sct::ProfScope _ps(name, strm);                            \
+    hipLaunchKernelGGL(kern, grid, block, 0, strm, __VA_ARGS__); \
+  } while (0);                                                   \
+  LAUNCHCHK()
+
+inline int bitlen(uint64_t v) {  // bits for ids 0..v-1; 0 when v <= 1
+  return v <= 1 ? 0 : 64 - __builtin_clzll(v - 1);
+}
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+template <typename T>
+inline T* at(void* ws, size_t off) {
+  return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
+}
+
+// ---------------- device helpers ----------------
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+  for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// exclusive scan over the kBlock threads of the block; *total gets the block sum.
+// `lds` needs kWaves + 1 entries.  Contains barriers: call from every thread.
+template <typename T>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* total, T* lds) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  T x = v;
+  for (int off = 1; off < kWave; off <<= 1) {
+    T y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == kWave - 1) lds[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T run = 0;
+    for (int w = 0; w < kWaves; w++) {
+      T t = lds[w];
+      lds[w] = run;
+      run += t;
+    }
+    lds[kWaves] = run;
+  }
+  __syncthreads();
+  T res = lds[wid] + x - v;
+  *total = lds[kWaves];
+  __syncthreads();
+  return res;
+}
+
+// a / b of two small non-negative integers, correctly rounded (Python int / int);
+// 0 for b == 0 (only reached by records the reference never aggregates)
+__device__ __forceinline__ double ratio(uint32_t a, uint32_t b) { return b ? (double)a / (double)b : 0.0; }
+
+__device__ __forceinline__ uint32_t frag_hash(int32_t ref, int32_t pos, uint32_t strand) {
+  uint32_t h = (uint32_t)ref * 0x9E3779B1u ^ ((uint32_t)pos * 0x85EBCA77u) ^ (strand * 0xC2B2AE3Du);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h;
+}
+
+}  // namespace sct
+
+namespace sct {
+
+// Wave-cooperative flush of per-lane partial sums into int64 rows.
+//
+// Lanes with `member` set hold partial sums v[0..K) for entity `e` (per lane).  For every
+// distinct entity among the members (a wave-uniform loop; one iteration when the wave
+// is inside one entity), the members' values are summed across the wave and lanes
+// 0..K-1 add slot SlotOf(i) of that entity's row with ONE atomic instruction (K
+// contiguous-ish int64 adds) instead of K single-lane instructions per lane.
+// Members' v[] are cleared.  Every lane of the wave must call it.
+template <int K, typename SlotOf>
+__device__ __forceinline__ void wave_flush(int64_t (&v)[K], bool member, int64_t e, int64_t* __restrict__ rows,
+                                           SlotOf slot_of) {
+  static_assert(K <= kWave, "one lane per slot");
+  const int lane = threadIdx.x & (kWave - 1);
+  uint64_t pending = __ballot(member);
+  while (pending) {
+    const int lead = __ffsll((unsigned long long)pending) - 1;
+    const int64_t el = __shfl(e, lead);
+    const bool in = member && e == el;
+    int64_t mine = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+      const int64_t tot = wave_sum(in ? v[i] : (int64_t)0);
+      mine = (lane == i) ? tot : mine;
+    }
+    if (lane < K && mine) atomicAdd((unsigned long long*)&rows[el * SCT_NP + slot_of(lane)], (unsigned long long)mine);
+    if (in) {
+#pragma unroll
+      for (int i = 0; i < K; i++) v[i] = 0;
+    }
+    pending &= ~__ballot(in);
+  }
+}
+
+}  // namespace sct

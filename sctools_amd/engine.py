@@ -85,8 +85,9 @@ class Engine:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def _plan(self, n, mode, float_mode, dims: Dims, max_entities=0) -> N.Plan:
+    def _plan(self, n, mode, float_mode, dims: Dims, max_entities=0, flags=0) -> N.Plan:
         p = N.Plan()
+        p.flags = int(flags)
         p.n_records = int(n)
         p.max_entities = int(max_entities)
         p.mode = MODES[mode]
@@ -150,6 +151,28 @@ class Engine:
         N.check(self.lib.sct_gene_partials(ctypes.byref(plan), ctypes.byref(rec), ctypes.c_void_p(ws.data_ptr()),
                                            ws.numel(), ctypes.c_void_p(out.data_ptr()), self._stream()))
         return out
+
+    def cell_and_gene(self, cols, dims: Dims, gene_is_mito: torch.Tensor, n_entities: Optional[int] = None,
+                      partials: Optional[torch.Tensor] = None):
+        """Cell rows (exact-sum floats) and grouped gene partials from one pass over cell-sorted records."""
+        rec = records_struct(cols)
+        if n_entities is None:
+            n_entities = self.count_entities(cols, "cell", dims)
+        cap = max(1, int(n_entities))
+        plan = self._plan(rec.n, "cell", "exact", dims, max_entities=cap, flags=N.PLAN_GENE_PARTIALS)
+        ws = self.workspace(plan)
+        ints = torch.empty((cap, N.SCT_NI), dtype=torch.int64, device=self.device)
+        floats = torch.empty((cap, N.SCT_NF), dtype=torch.float64, device=self.device)
+        if partials is None:
+            partials = torch.empty((max(1, dims.n_gene_ids), N.SCT_NP), dtype=torch.int64, device=self.device)
+        rows = ctypes.c_int64(0)
+        N.check(self.lib.sct_cell_metrics_gene_partials(
+            ctypes.byref(plan), ctypes.byref(rec), ctypes.c_void_p(gene_is_mito.data_ptr()),
+            ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(ints.data_ptr()),
+            ctypes.c_void_p(floats.data_ptr()), cap, ctypes.byref(rows), ctypes.c_void_p(partials.data_ptr()),
+            self._stream()))
+        r = int(rows.value)
+        return ints[:r], floats[:r], partials
 
     def finalize_partials(self, partials: torch.Tensor, mode: str = "gene_grouped"):
         rows = int(partials.shape[0])

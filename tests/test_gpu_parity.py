@@ -167,3 +167,36 @@ def test_properties_at_scale(eng):
     a, b = wf.cpu().numpy(), cf.cpu().numpy()
     ok = np.isclose(a, b, rtol=REL, atol=0) | (np.isnan(a) & np.isnan(b))
     assert ok.all()
+
+
+def test_combined_cell_and_gene_pass(eng):
+    """sct_cell_metrics_gene_partials == separate cell rows + grouped gene partials."""
+    from sctools_amd import engine as E
+
+    d = gpu_synth(1_000_000, 150, 8_000, 41, p_none_cell_reads=0.01)
+    dims = E.Dims(d.n_cell_ids, d.n_gene_ids, d.n_umi_ids)
+    mito = torch.from_numpy(d.gene_is_mito).to(eng.device)
+    ci, cf, part = eng.cell_and_gene(d.cols, dims, mito)
+    ci2, cf2 = eng.compute(d.cols, "cell", dims, mito, mito, float_mode="exact")
+    part2 = eng.gene_partials(d.cols, dims)
+    assert torch.equal(ci, ci2)
+    assert torch.equal(torch.nan_to_num(cf, 3.0), torch.nan_to_num(cf2, 3.0))
+    assert torch.equal(part, part2)
+    h = host_cols(d)
+    oi, of = O.run(h, "gene_grouped", d.gene_is_mito, d.n_gene_ids, threads=8)
+    gi, gf = eng.finalize_partials(part)
+    gi, gf = gi.cpu().numpy(), gf.cpu().numpy()
+    live = oi[:, 0] > 0
+    compare(gi[live], gf[live], oi[live], of[live], exact_floats=False)
+
+
+def test_grouped_needs_cell_sorted_input(eng):
+    from sctools_amd import _native as N
+
+    cols = H.bam_columns("unsorted", "cell")
+    d = dims_of(len(cols.cells), len(cols.genes), len(cols.umis))
+    from sctools_amd import engine as E
+
+    dev = E.to_device(cols.arrays, eng.device)
+    with pytest.raises(N.EngineError, match="cell-sorted"):
+        eng.gene_partials(dev, d)
