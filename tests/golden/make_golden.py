@@ -161,6 +161,33 @@ def main():
         run_ref(GatherGeneMetrics, src, os.path.join(HERE, "ref", stem + ".gene.csv"))
         print("reference outputs for", b)
 
+    # 2b. reference merges of two overlapping 75 % halves of a metric CSV (the reference's
+    # own multi-chunk emulation, test_metrics.py:812-838)
+    from sctools.metrics.merge import MergeCellMetrics, MergeGeneMetrics
+
+    os.makedirs(os.path.join(HERE, "merge"), exist_ok=True)
+    for kind, src, merger in (("cell", "small-cell-sorted.cell.csv", MergeCellMetrics),
+                              ("gene", "small-gene-sorted.gene.csv", MergeGeneMetrics)):
+        lines = open(os.path.join(HERE, "ref", src)).read().splitlines()
+        header, data = lines[0], lines[1:]
+        lo, hi = round(len(data) * 0.25), round(len(data) * 0.75)
+        parts = []
+        for k, chunk in enumerate((data[:hi], data[lo:])):
+            fn = os.path.join(HERE, "merge", "%s_part%d.csv" % (kind, k + 1))
+            with open(fn, "w") as f:
+                f.write("\n".join([header] + chunk) + "\n")
+            parts.append(fn)
+        out = os.path.join(HERE, "merge", "%s_merged" % kind)
+        merger(parts, out).execute()
+        import gzip as _gz
+
+        with _gz.open(out + ".csv.gz", "rt") as f:
+            text = f.read()
+        os.remove(out + ".csv.gz")
+        with open(out + ".csv", "w") as f:
+            f.write(text)
+        print("reference merge", kind)
+
     # 3. synthetic columnar sets
     manifest = {}
     for name, (kw, shuffle_seed) in SYNTH_SETS.items():
