@@ -43,6 +43,11 @@ ALG_BYTES = {
 }
 
 
+def pipeline_bytes(prof, args):
+    passes = prof.get("radix_downsweep", (0.0, 0))[1] / max(1, args.steps)
+    return 32 + 12 + 24 * passes + 44
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -75,6 +80,7 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
 
+    from sctools_amd import distributed as D
     from sctools_amd import engine as E
     from sctools_amd import synth
 
@@ -103,8 +109,7 @@ def main():
         else:
             ci, cf = eng.compute(data.cols, "cell", dims, mito, multi, float_mode=args.float_mode, n_entities=n_ent)
             eng.gene_partials(data.cols, dims, out=partials)
-        if world > 1:
-            dist.all_reduce(partials, op=dist.ReduceOp.SUM)
+        D.allreduce_partials(partials)  # RCCL over xGMI when N > 1; no-op at N = 1
         gi, gf = eng.finalize_partials(partials)
         host_cells[: ci.shape[0]].copy_(ci, non_blocking=True)
         host_cellf[: cf.shape[0]].copy_(cf, non_blocking=True)
@@ -158,6 +163,9 @@ def main():
         "avg_launch_ms": avg_s * 1e3,
         "launches_per_step": dom_launches / args.steps,
         "alg_bytes_per_record": ALG_BYTES.get(dom_name, 0),
+        # whole pipeline against SURVEY.md 8(d)'s B_alg = 32 + 12 + 24*P + 44 bytes/record
+        "pipeline_alg_bytes_per_record": pipeline_bytes(prof, args),
+        "pipeline_frac": value / world * pipeline_bytes(prof, args) / PEAK_HBM,
     }
     kernel_ms_per_step = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}
 

@@ -1,0 +1,108 @@
+"""
+Multi-GPU cell + gene metrics: one process per GPU, cells sharded across ranks.
+
+The reference scales this path by splitting the BAM into cell-disjoint chunks
+(``SplitBam``, ``/root/reference/src/sctools/bam.py:263-410``), running the
+gatherer on each chunk and merging the CSVs (``MergeCellMetrics`` concatenates,
+``MergeGeneMetrics`` folds, ``metrics/merge.py:66-209``).  Here the same
+invariant -- no cell spans two shards -- gives:
+
+* cell rows: each rank's rows are final; rank order = record order, so the
+  rows are gathered to one rank and concatenated (the MergeCellMetrics step);
+* gene rows: each rank produces additive per-gene partial rows (int64 counters
+  and exact-sum lanes, ``include/sctools_gpu.h`` SCT_NP layout).  Because
+  molecules, fragments and cells of a gene are keyed by cell, distinct counts
+  of disjoint cell sets add; so ONE all-reduce(SUM) of the [n_gene_ids, 64]
+  int64 block followed by the finalize kernel gives exactly the unsharded gene
+  rows (the MergeGeneMetrics step, without its weighted-mean approximation).
+
+The all-reduce is the only data-path collective (RCCL over xGMI with the
+``nccl`` backend; the CPU tests drive the same code with ``gloo``).
+"""
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from sctools_amd import _native as N
+
+
+def shard_bounds(entity, world: int) -> List[Tuple[int, int]]:
+    """Split records [0, n) into ``world`` contiguous ranges, balanced by record count,
+    cutting only at entity-run boundaries (a run never spans two ranges)."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    e = entity if isinstance(entity, torch.Tensor) else torch.as_tensor(np.asarray(entity))
+    n = int(e.numel())
+    if n == 0:
+        return [(0, 0)] * world
+    heads = (torch.nonzero(e[1:] != e[:-1]).flatten() + 1).cpu()
+    cuts = [0]
+    for r in range(1, world):
+        t = (n * r + world - 1) // world
+        j = int(torch.searchsorted(heads, torch.tensor([t], dtype=heads.dtype)).item())
+        c = int(heads[j].item()) if j < heads.numel() else n
+        cuts.append(max(c, cuts[-1]))
+    cuts.append(n)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def shard(cols, lo: int, hi: int):
+    """The record range [lo, hi) of every column (contiguous views)."""
+    return {k: v[lo:hi] for k, v in cols.items()}
+
+
+def allreduce_partials(partials: torch.Tensor, group=None) -> torch.Tensor:
+    """Sum the per-gene partial rows of every rank in place (int64: exact, order-free)."""
+    if partials.dtype != torch.int64:
+        raise TypeError("partials must be int64")
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(partials, op=dist.ReduceOp.SUM, group=group)
+    return partials
+
+
+def gather_rows(tensors: Sequence[torch.Tensor], dst: int = 0, group=None) -> Optional[List[torch.Tensor]]:
+    """Concatenate each [rows_r, k] tensor over ranks in rank order; result on ``dst`` only."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return list(tensors)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = tensors[0].device
+    cnt = torch.tensor([tensors[0].shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    top = max(max(counts), 1)
+    out = []
+    for t in tensors:
+        pad = torch.zeros((top,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+        pad[: t.shape[0]] = t
+        bufs = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(bufs, pad, group=group)
+        out.append(torch.cat([b[:c] for b, c in zip(bufs, counts)]) if rank == dst else None)
+    return out if rank == dst else None
+
+
+class ShardedCellGeneMetrics:
+    """Cell rows + grouped gene rows of a cell-sharded record set.
+
+    ``backend`` is the engine (``sctools_amd.engine.Engine``): it provides
+    ``cell_and_gene(cols, dims, mito, n_entities=None, partials=None)`` and
+    ``finalize_partials(partials)``.  Each rank calls :meth:`run` on its shard.
+    """
+
+    def __init__(self, backend, group=None, dst: int = 0):
+        self.backend = backend
+        self.group = group
+        self.dst = dst
+
+    def run(self, shard_cols, dims, gene_is_mito, record_offset: int = 0, partials=None):
+        ci, cf, part = self.backend.cell_and_gene(shard_cols, dims, gene_is_mito, partials=partials)
+        allreduce_partials(part, self.group)
+        gi, gf = self.backend.finalize_partials(part)
+        ci = ci.clone()
+        ci[:, N.I_ENTITY] += record_offset  # first-record index in the whole record set
+        cells = gather_rows([ci, cf], self.dst, self.group)
+        return (cells[0], cells[1]) if cells is not None else (None, None), (gi, gf)

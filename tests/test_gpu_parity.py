@@ -200,3 +200,32 @@ def test_grouped_needs_cell_sorted_input(eng):
     dev = E.to_device(cols.arrays, eng.device)
     with pytest.raises(N.EngineError, match="cell-sorted"):
         eng.gene_partials(dev, d)
+
+
+@pytest.mark.parametrize("name", ["s0", "s1", "s2"])
+def test_sharded_partials_add_up(eng, name):
+    """Cell-sharded partial rows summed (what the RCCL all-reduce does) finalize to exactly the
+    unsharded gene rows -- floats included, since exact-sum lanes are order-free integers."""
+    from sctools_amd import distributed as D
+    from sctools_amd import engine as E
+
+    s = H.synth(name)
+    d = dims_of(*s.dims)
+    cols = E.to_device(s.arrays, eng.device)
+    gm = torch.from_numpy(s.gene_is_mito).to(eng.device)
+    ci, cf, whole = eng.cell_and_gene(cols, d, gm)
+    wi, wf = eng.finalize_partials(whole.clone())
+    acc = torch.zeros_like(whole)
+    rows_i, rows_f = [], []
+    for lo, hi in D.shard_bounds(cols["cell"], 3):
+        si, sf, p = eng.cell_and_gene(D.shard(cols, lo, hi), d, gm)
+        si = si.clone()
+        si[:, 23] += lo
+        rows_i.append(si)
+        rows_f.append(sf.clone())
+        acc += p
+    gi, gf = eng.finalize_partials(acc)
+    assert torch.equal(gi, wi)
+    assert torch.equal(gf.view(torch.int64), wf.view(torch.int64))
+    assert torch.equal(torch.cat(rows_i), ci)
+    assert torch.equal(torch.cat(rows_f).view(torch.int64), cf.view(torch.int64))
