@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(kBlock) k_reduce_sorted(const uint64_t* __rest
   __shared__ uint64_t s_k[kReduceTile + 2];
   __shared__ uint32_t s_v[kReduceTile];
   const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kReduceTile;
+  const int64_t base = (int64_t)xcd_tile(blockIdx.x, gridDim.x) * kReduceTile;
   const int tile_n = (int)((n - base) < kReduceTile ? (n - base) : kReduceTile);
   for (int q = t; q < tile_n; q += kBlock) {
     s_k[q + 1] = keys[base + q];

@@ -95,6 +95,18 @@ inline T* at(void* ws, size_t off) {
 }
 
 // ---------------- device helpers ----------------
+constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, each with its own (non-coherent) 4 MiB L2
+
+// Workgroups are dispatched round-robin over the XCDs (block b -> XCD b % 8).  Map them to
+// logical tiles so that each XCD owns one contiguous range of tiles: neighbouring tiles
+// (same entity, same record-index window) then share an L2, so scattered writes and
+// gathers into that window combine there instead of leaving partial lines in 8 L2s.
+__device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned n) {
+  const unsigned x = b % kXcds, i = b / kXcds;
+  const unsigned per = n / kXcds, rem = n % kXcds;
+  return x * per + (x < rem ? x : rem) + i;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
   for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);

@@ -1,0 +1,48 @@
+"""Workload for rocprofv3 --pmc passes (HBM traffic per kernel).
+
+Runs the bench step (cell + grouped gene metrics, exact mode) on the config-2
+shard twice, then a calibration copy of a known byte count (torch clone of a
+1 GiB int64 tensor: 1 GiB read + 1 GiB written with wide coalesced accesses),
+so the counters' units and the gfx950 FETCH_SIZE correction can be checked
+against a known figure in the same run.  Run under rocprofv3, e.g.
+
+  rocprofv3 --pmc FETCH_SIZE --output-format csv -d OUT -o fetch -- python3 tools/pmc_probe.py
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=100_000_000)
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    from sctools_amd import engine as E
+    from sctools_amd import synth
+
+    dev = torch.device("cuda", 0)
+    eng = E.get_engine(dev)
+    data = synth.generate(synth.SynthConfig(n_reads=a.records, n_cells=10_000, n_genes=30_000, sigma=1.0, seed=0),
+                          device=dev, chunk=16_000_000)
+    dims = E.Dims(data.n_cell_ids, data.n_gene_ids, data.n_umi_ids)
+    mito = torch.from_numpy(data.gene_is_mito).to(dev)
+    n_ent = eng.count_entities(data.cols, "cell", dims)
+    for _ in range(a.reps):
+        ci, cf, part = eng.cell_and_gene(data.cols, dims, mito, n_entities=n_ent)
+        eng.finalize_partials(part)
+    torch.cuda.synchronize()
+    x = torch.ones(1 << 27, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    y = x.clone()
+    torch.cuda.synchronize()
+    print("calibration clone bytes read=%d written=%d" % (x.numel() * 8, y.numel() * 8), flush=True)
+
+
+if __name__ == "__main__":
+    main()
