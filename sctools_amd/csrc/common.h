@@ -40,9 +40,13 @@ static_assert(SCT_P_FLOAT_BASE + kStreams * 8 <= SCT_NP, "partials row too small
 
 constexpr uint32_t kUnmappedValBit = 0x80000000u;  // sort value bit 31: the record is unmapped
 
-struct Bits {  // key layout: [entity | k1 | k2 | hash]
+struct Bits {  // key layout: [entity | k1' | k2 | hash], k1' = k1 * mul mod 2^k1 (a bijection)
   int e, k1, k2, h;
+  uint32_t mul = 1, inv = 1;  // odd multiplier and its inverse mod 2^k1 (1, 1: identity)
   int total() const { return e + k1 + k2 + h; }
+  __host__ __device__ uint32_t k1_mask() const { return k1 ? (uint32_t)((1ull << k1) - 1) : 0u; }
+  __host__ __device__ uint32_t scramble(uint32_t k) const { return (k * mul) & k1_mask(); }
+  __host__ __device__ uint32_t unscramble(uint32_t k) const { return (k * inv) & k1_mask(); }
 };
 
 }  // namespace sct

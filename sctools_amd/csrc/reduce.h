@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(kBlock) k_reduce_sorted(const uint64_t* __rest
     acc[4] += k1_head;
     acc[5] += k1_multi;
     if constexpr (kCell) {
-      if (k1_head) acc[6] += k1_is_mito[(uint32_t)((k >> sh_k1) & k1_mask)];
+      if (k1_head) acc[6] += k1_is_mito[b.unscramble((uint32_t)((k >> sh_k1) & k1_mask))];
     }
     if (mapped) {
       bool is_first = true, single = true;

@@ -8,22 +8,25 @@
 //   segment.h   entity runs (bam.iter_tag_groups, bam.py:492-540) and packed
 //               64-bit keys [run | k1 | k2 | fragment hash], bits trimmed to the
 //               dictionary sizes (cell: k1 = gene, k2 = umi; gene: k1 = cell)
-//   radix.h     LSD radix sort of (key, record index), LDS-staged tiles,
-//               wave-level multi-split ranking, coalesced bucket writes
-//   reduce.h    one pass over the sorted keys: Counter results from key runs,
-//               per-record metrics into int64 partial rows, and (cell view) a
-//               16-byte gene contribution per record into its gene bucket
+//   bucket.h    distinct counts: per-entity MSD bucket partition of the keys
+//               [k1 | k2 | fragment hash] until every bucket fits a tile, then an
+//               LDS sort + neighbour pass per tile (the default path)
+//   radix.h     device-wide LSD radix sort of (key, record index) -- the path for
+//               keys too wide for bucket.h (k1 + k2 > 40 bits)
+//   reduce.h    one pass over the globally sorted keys: Counter results from key runs
 //   gene.h      gene buckets -> per-gene partial rows (LDS bins)
 //   finalize.h  partial rows -> output rows; sequential Welford float path
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared.
 // -ffp-contract=off keeps every Welford operation separately rounded, as Python does.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "common.h"
 #include "finalize.h"
 #include "fixedpt.h"
+#include "bucket.h"
 #include "gene.h"
 #include "radix.h"
 #include "reduce.h"
@@ -36,8 +39,9 @@ namespace {
 
 struct Layout {
   size_t tile_cnt, scalars, scan_sums, keys_a, keys_b, vals_a, vals_b, counts, offsets, ent_start, partials;
-  size_t gcounts, goffsets, gsums, gwork, dflags, gpay, seen, zero_mito, total;
-  int64_t num_tiles, num_chunks, max_ent, max_gene_work, gene_cells;
+  size_t gcounts, goffsets, gsums, gwork, dflags, gpay, seen, zero_mito;
+  size_t bdesc, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, total;
+  int64_t num_tiles, num_chunks, max_ent, max_gene_work, gene_cells, max_seg, max_work;
   int n_buckets;
   bool gene;
 };
@@ -80,6 +84,17 @@ Layout layout_for(const sct_plan_t* plan) {
   L.gpay = take(L.gene ? sizeof(GenePayload) * (size_t)n1 : 0);
   L.seen = take(L.gene ? sizeof(uint32_t) * (size_t)(plan->n_cell_ids > 0 ? plan->n_cell_ids : 1) : 0);
   L.zero_mito = take(L.gene ? (size_t)(plan->n_gene_ids > 0 ? plan->n_gene_ids : 1) : 0);
+  // bucket.h: segments have > kBCap records and are disjoint within a level (and giants overall)
+  L.max_seg = n1 / (kBCap + 1) + 2;
+  L.max_work = n1 / kChunk + L.max_seg + 2;
+  L.bdesc = take(sizeof(uint16_t) * (size_t)n1);
+  L.seg_a = take(sizeof(Seg) * (size_t)L.max_seg);
+  L.seg_b = take(sizeof(Seg) * (size_t)L.max_seg);
+  L.work_a = take(sizeof(Work) * (size_t)L.max_work);
+  L.work_b = take(sizeof(Work) * (size_t)L.max_work);
+  L.seg_hist = take(sizeof(uint32_t) * kRadix * (size_t)L.max_seg);
+  L.seg_cur = take(sizeof(uint32_t) * kRadix * (size_t)L.max_seg);
+  L.giants = take(sizeof(Seg) * (size_t)L.max_seg);
   L.total = off;
   return L;
 }
@@ -138,6 +153,91 @@ int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool du
   return SCT_OK;
 }
 
+// bucket.h driver: level 0 classification, MSD levels until no segment exceeds kBCap, then
+// the tile pass (+ giants).  One host sync per level to size the next level's launches.
+int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const int64_t* ent_start, RecCols r,
+                    const uint8_t* mito, const Bits& b, bool cell, bool gene, int64_t* partials, uint16_t* dflags,
+                    hipStream_t s) {
+  if (n == 0) return SCT_OK;
+  uint64_t* ka = at<uint64_t>(ws, L.keys_a);
+  uint64_t* kb = at<uint64_t>(ws, L.keys_b);
+  uint32_t* va = at<uint32_t>(ws, L.vals_a);
+  uint32_t* vb = at<uint32_t>(ws, L.vals_b);
+  uint16_t* bdesc = at<uint16_t>(ws, L.bdesc);
+  Seg* seg[2] = {at<Seg>(ws, L.seg_a), at<Seg>(ws, L.seg_b)};
+  Work* work[2] = {at<Work>(ws, L.work_a), at<Work>(ws, L.work_b)};
+  uint32_t* hist = at<uint32_t>(ws, L.seg_hist);
+  uint32_t* cur = at<uint32_t>(ws, L.seg_cur);
+  Seg* giants = at<Seg>(ws, L.giants);
+  BucketCtl* ctl = reinterpret_cast<BucketCtl*>(at<uint64_t>(ws, L.scalars) + 8);
+  const int KB = b.k1 + b.k2 + b.h;
+  HIPCHK(hipMemsetAsync(bdesc, 0, sizeof(uint16_t) * (size_t)n, s));
+  HIPCHK(hipMemsetAsync(ctl, 0, sizeof(BucketCtl), s));
+  LAUNCH("bucket_level0", k_bucket_level0, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, ent_start, n_ent, n,
+         bdesc, seg[0], work[0], ctl);
+  BucketCtl h{};
+  HIPCHK(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  int depth = 0, level = 1, c = 0;
+  while (h.n_seg > 0) {
+    if ((int64_t)h.n_seg > L.max_seg || (int64_t)h.n_work > L.max_work)
+      return fail(SCT_ENOMEM, "bucket level %d: %u segments / %u work items exceed the workspace", level, h.n_seg,
+                  h.n_work);
+    const int bits = KB - depth < kRadixBits ? KB - depth : kRadixBits;
+    const int shift = KB - depth - bits;
+    const int src = (level - 1) & 1;
+    const uint64_t* kin = src ? kb : ka;
+    const uint32_t* vin = src ? vb : va;
+    uint64_t* kout = src ? ka : kb;
+    uint32_t* vout = src ? va : vb;
+    HIPCHK(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kRadix * (size_t)h.n_seg, s));
+    LAUNCH("bucket_hist", k_bucket_hist, dim3(h.n_work), dim3(kBlock), s, kin, (const Seg*)seg[c],
+           (const Work*)work[c], shift, bits, hist);
+    LAUNCH("bucket_segscan", k_bucket_segscan, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c],
+           (const uint32_t*)hist, cur);
+    LAUNCH("bucket_scatter", k_bucket_scatter, dim3(h.n_work), dim3(kBlock), s, kin, vin, kout, vout,
+           (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
+    HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), s));  // next level's n_seg, n_work
+    LAUNCH("bucket_classify", k_bucket_classify, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c],
+           (const uint32_t*)hist, (const uint32_t*)cur, depth, bits, b.k1, b.k1 + b.k2, KB, level & 1, bdesc,
+           seg[c ^ 1], work[c ^ 1], giants, ctl);
+    HIPCHK(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    c ^= 1;
+    depth += bits;
+    level++;
+  }
+  const int64_t n_win = cdiv(n, kWin);
+  uint32_t* win_ent = at<uint32_t>(ws, L.counts);  // the global-sort count matrix is unused here
+  LAUNCH("bucket_windows", k_window_entities, dim3((unsigned)cdiv(n_win + 1, kBlock)), dim3(kBlock), s, ent_start,
+         n_ent, n, n_win, win_ent);
+  const dim3 tgrid((unsigned)n_win);
+  if (cell && gene) {
+    LAUNCH("bucket_tile", (k_bucket_tile<true, true>), tgrid, dim3(kBlock), s, (const uint16_t*)bdesc, ka, va, kb,
+           vb, n, ent_start, (const uint32_t*)win_ent, r, mito, b, partials, dflags);
+  } else if (cell) {
+    LAUNCH("bucket_tile", (k_bucket_tile<true, false>), tgrid, dim3(kBlock), s, (const uint16_t*)bdesc, ka, va, kb,
+           vb, n, ent_start, (const uint32_t*)win_ent, r, mito, b, partials, dflags);
+  } else {
+    LAUNCH("bucket_tile", (k_bucket_tile<false, false>), tgrid, dim3(kBlock), s, (const uint16_t*)bdesc, ka, va,
+           kb, vb, n, ent_start, (const uint32_t*)win_ent, r, mito, b, partials, dflags);
+  }
+  if (h.n_giant > 0) {
+    const dim3 ggrid(h.n_giant);
+    if (cell && gene) {
+      LAUNCH("bucket_giant", (k_bucket_giant<true, true>), ggrid, dim3(kBlock), s, (const Seg*)giants, ka, va, kb,
+             vb, r, mito, b, partials, dflags);
+    } else if (cell) {
+      LAUNCH("bucket_giant", (k_bucket_giant<true, false>), ggrid, dim3(kBlock), s, (const Seg*)giants, ka, va, kb,
+             vb, r, mito, b, partials, dflags);
+    } else {
+      LAUNCH("bucket_giant", (k_bucket_giant<false, false>), ggrid, dim3(kBlock), s, (const Seg*)giants, ka, va, kb,
+             vb, r, mito, b, partials, dflags);
+    }
+  }
+  return SCT_OK;
+}
+
 // The RUN-mode pipeline (entity = runs of the cell column, or of the gene column in gene
 // mode; GROUPED runs the cell view).  Writes partial rows into the workspace, output rows
 // if out_i / out_f are set, and grouped gene partials (cell view) if gene_partials is set.
@@ -162,16 +262,34 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   if (out_i && n_ent > capacity)
     return fail(SCT_EINVAL, "%lld entities exceed output capacity %lld", (long long)n_ent, (long long)capacity);
 
+  // key bits.  Bucket path (default): [k1' | k2 | hash], KB <= kMaxKeyBits, entities implied by
+  // the record ranges.  Global-sort path: [run | k1' | k2 | hash], padded to whole radix digits.
   Bits b;
-  b.e = bitlen((uint64_t)n_ent);
   b.k1 = bitlen((uint64_t)(cell ? plan->n_gene_ids : plan->n_cell_ids));
   b.k2 = bitlen((uint64_t)plan->n_umi_ids);
-  const int used = b.e + b.k1 + b.k2;
-  if (used > 63) return fail(SCT_EINVAL, "packed key needs %d bits (> 63)", used);
-  // fill the last radix digit with fragment-hash bits (same pass count), every shift < 64
-  const int padded = ((used + kRadixBits - 1) / kRadixBits) * kRadixBits;
-  b.h = (padded > 63 ? 63 : padded) - used;
-  if (b.h > 32) b.h = 32;
+  const char* force = getenv("SCT_FORCE_GLOBAL_SORT");
+  const bool bucket = b.k1 + b.k2 <= kMaxKeyBits && !(force && force[0] == '1');
+  int used;
+  if (bucket) {
+    b.e = 0;
+    used = b.k1 + b.k2;
+    b.h = kMaxKeyBits - used < 8 ? kMaxKeyBits - used : 8;
+  } else {
+    b.e = bitlen((uint64_t)n_ent);
+    used = b.e + b.k1 + b.k2;
+    if (used > 63) return fail(SCT_EINVAL, "packed key needs %d bits (> 63)", used);
+    // fill the last radix digit with fragment-hash bits (same pass count), every shift < 64
+    const int padded = ((used + kRadixBits - 1) / kRadixBits) * kRadixBits;
+    b.h = (padded > 63 ? 63 : padded) - used;
+    if (b.h > 32) b.h = 32;
+  }
+  if (b.k1 > 0) {  // spread neighbouring k1 ids over the top key digits (odd multiplier, bijective)
+    b.mul = 0x9E3779B1u & b.k1_mask();
+    b.mul |= 1u;
+    uint32_t inv = b.mul;  // Newton: inverse mod 2^32, then mod 2^k1
+    for (int it = 0; it < 5; it++) inv *= 2u - b.mul * inv;
+    b.inv = inv & b.k1_mask();
+  }
 
   KeyCols kc{ent_col, cell ? rec->gene : rec->cell, rec->umi};
   RecCols rc2{rec->ref, rec->pos, rec->gq_sum, rec->gq_len, rec->gq_gt30, rec->bits, rec->xf,
@@ -212,25 +330,28 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     }
   }
 
-  // 2. sort (key, value)
-  int which = 0;
-  rc = radix_sort(B, n, used + b.h, &which, s);
-  if (rc) return rc;
-  const uint64_t* keys = which ? B.kb : B.ka;
-  const uint32_t* vals = which ? B.vb : B.va;
-
-  // 3. sorted order: distinct counts (+ per-record distinct events for the gene view)
+  // 2-3. distinct counts (+ per-record distinct events for the gene view)
   uint16_t* dflags = gene ? at<uint16_t>(ws, L.dflags) : nullptr;
-  const dim3 rgrid((unsigned)cdiv(n, kReduceTile));
-  if (cell && gene) {
-    LAUNCH("reduce_sorted", (k_reduce_sorted<true, true>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
-           partials, dflags);
-  } else if (cell) {
-    LAUNCH("reduce_sorted", (k_reduce_sorted<true, false>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
-           partials, dflags);
+  if (bucket) {
+    rc = bucket_distinct(L, ws, n, n_ent, ent_start, rc2, mito, b, cell, gene, partials, dflags, s);
+    if (rc) return rc;
   } else {
-    LAUNCH("reduce_sorted", (k_reduce_sorted<false, false>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
-           partials, dflags);
+    int which = 0;
+    rc = radix_sort(B, n, used + b.h, &which, s);
+    if (rc) return rc;
+    const uint64_t* keys = which ? B.kb : B.ka;
+    const uint32_t* vals = which ? B.vb : B.va;
+    const dim3 rgrid((unsigned)cdiv(n, kReduceTile));
+    if (cell && gene) {
+      LAUNCH("reduce_sorted", (k_reduce_sorted<true, true>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
+             partials, dflags);
+    } else if (cell) {
+      LAUNCH("reduce_sorted", (k_reduce_sorted<true, false>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
+             partials, dflags);
+    } else {
+      LAUNCH("reduce_sorted", (k_reduce_sorted<false, false>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
+             partials, dflags);
+    }
   }
 
   if (out_i) {

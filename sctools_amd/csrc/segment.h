@@ -56,7 +56,8 @@ struct KeyCols {
 
 __device__ __forceinline__ uint64_t make_key(uint64_t e, uint32_t k1, uint32_t k2, uint32_t hash, const Bits& b) {
   const uint64_t hv = b.h ? (uint64_t)(hash >> (32 - b.h)) : 0;  // top bits of the fragment mix
-  return (e << (b.k1 + b.k2 + b.h)) | ((uint64_t)k1 << (b.k2 + b.h)) | ((uint64_t)k2 << b.h) | hv;
+  const uint64_t ev = b.e ? (e << (b.k1 + b.k2 + b.h)) : 0;  // bucket path: entities are record ranges
+  return ev | ((uint64_t)b.scramble(k1) << (b.k2 + b.h)) | ((uint64_t)k2 << b.h) | hv;
 }
 
 // per-record additive counters of one run

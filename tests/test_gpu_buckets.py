@@ -1,0 +1,172 @@
+"""Edge cases of the bucket path (sctools_amd/csrc/bucket.h) against the oracle.
+
+Records are crafted so that every branch of the MSD partition runs:
+* a k1 value (gene of a cell) with > 2047 reads, split over sibling buckets (k1 split flags);
+* a molecule with > 2047 reads over many positions, split on fragment-hash bits (molecule flags);
+* a molecule with > 2047 reads at ONE fragment: a giant bucket (whole key fixed);
+* a giant holding two different fragments whose hashes collide in the key's hash bits,
+  plus unmapped records (the exact fragment loop);
+* thousands of tiny entities (many buckets per tile);
+both with narrow dictionaries (the k1 boundary inside the first digit) and wide ones.
+The global-sort path (SCT_FORCE_GLOBAL_SORT=1) must give identical rows.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-9
+M32 = 0xFFFFFFFF
+
+
+def frag_hash(ref, pos, strand):
+    """util.h frag_hash, for crafting top-bit collisions."""
+    h = ((ref * 0x9E3779B1) ^ (pos * 0x85EBCA77) ^ (strand * 0xC2B2AE3D)) & M32
+    h ^= h >> 15
+    h = (h * 0x2C1B3C6D) & M32
+    h ^= h >> 12
+    h = (h * 0x297A2D39) & M32
+    h ^= h >> 15
+    return h
+
+
+def bitlen(v):
+    return 0 if v <= 1 else int(v - 1).bit_length()
+
+
+def colliding_pos(ref, pos, hbits, start=5000):
+    want = frag_hash(ref & M32, pos, 0) >> (32 - hbits)
+    p = start
+    while True:
+        if p != pos and frag_hash(ref & M32, p, 0) >> (32 - hbits) == want:
+            return p
+        p += 1
+
+
+def craft(n_gene_ids, n_umi_ids, seed):
+    rng = np.random.default_rng(seed)
+    hbits = min(8, 40 - bitlen(n_gene_ids) - bitlen(n_umi_ids))
+    rows = []  # (cell, gene, umi, ref, pos, unmapped)
+
+    def add(cell, gene, umi, ref, pos, unmapped=False, k=1):
+        for _ in range(k):
+            rows.append((cell, gene, umi, ref, pos, unmapped))
+
+    g_heavy = n_gene_ids - 3
+    # cell 0: background + a giant molecule at one fragment + a colliding-hash giant + unmapped reads
+    for _ in range(2000):
+        add(0, int(rng.integers(1, n_gene_ids)), int(rng.integers(0, n_umi_ids)), int(rng.integers(0, 25)),
+            int(rng.integers(0, 1 << 20)))
+    add(0, g_heavy, 5, 1, 1000, k=2600)
+    p2 = colliding_pos(3, 777, hbits)
+    add(0, g_heavy, 6, 3, 777, k=1300)
+    add(0, g_heavy, 6, 3, p2, k=1200)
+    add(0, g_heavy, 6, 3, 777, k=1)
+    add(0, g_heavy, 6, -1, -1, unmapped=True, k=40)
+    # cell 1: one gene with 5000 reads over 12 UMIs (k1 split) at random positions
+    for _ in range(5000):
+        add(1, 7 % n_gene_ids, int(rng.integers(0, 12)), 2, int(rng.integers(0, 1 << 16)))
+    # cell 2: one molecule with 3000 reads over 400 positions (molecule split on hash bits)
+    for _ in range(3000):
+        add(2, 9 % n_gene_ids, 3, 4, int(rng.integers(0, 400)) * 10)
+    # cells 3..: thousands of tiny cells (1-4 reads)
+    c = 3
+    for _ in range(4000):
+        for _ in range(int(rng.integers(1, 5))):
+            add(c, int(rng.integers(0, n_gene_ids)), int(rng.integers(0, n_umi_ids)), int(rng.integers(0, 25)),
+                int(rng.integers(0, 1 << 20)), unmapped=bool(rng.random() < 0.05))
+        c += 1
+    a = np.array(rows, dtype=np.int64)
+    # shuffle within cells (input order inside an entity is arbitrary)
+    order = np.lexsort((rng.random(len(a)), a[:, 0]))
+    a = a[order]
+    n = len(a)
+    unm = a[:, 5].astype(bool)
+    bits = np.where(unm, 1, 0) | np.where(rng.random(n) < 0.5, 2, 0)
+    bits[(a[:, 0] == 0) & (a[:, 1] == g_heavy)] &= ~2  # giants on the + strand (crafted positions)
+    bits |= np.where(~unm & (rng.random(n) < 0.3), 4, 0) | np.where(~unm & (rng.random(n) < 0.1), 8, 0)
+    bits |= np.where(~unm & (rng.random(n) < 0.8), 16, 0) | np.where(rng.random(n) < 0.9, 32, 0)
+    bits |= 64 | np.where(rng.random(n) < 0.95, 128, 0)
+    glen = rng.integers(30, 99, n)
+    arrays = {
+        "cell": a[:, 0].astype(np.int32), "umi": a[:, 2].astype(np.int32), "gene": a[:, 1].astype(np.int32),
+        "ref": np.where(unm, -1, a[:, 3]).astype(np.int32), "pos": np.where(unm, -1, a[:, 4]).astype(np.int32),
+        "gq_len": glen.astype(np.uint16), "gq_sum": (glen * rng.integers(20, 40, n)).astype(np.uint16),
+        "gq_gt30": rng.integers(0, glen + 1).astype(np.uint16), "bits": bits.astype(np.uint8),
+        "xf": np.where(unm, 0, rng.integers(1, 5, n)).astype(np.uint8),
+        "cy_len": np.full(n, 16, np.uint8), "cy_gt30": rng.integers(0, 17, n).astype(np.uint8),
+        "uy_len": np.full(n, 10, np.uint8), "uy_gt30": rng.integers(0, 11, n).astype(np.uint8),
+    }
+    mito = np.zeros(n_gene_ids, np.uint8)
+    mito[[7 % n_gene_ids, g_heavy]] = 1
+    return arrays, mito, int(a[:, 0].max()) + 1
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from sctools_amd import engine as E
+
+    return E.get_engine("cuda:0")
+
+
+def compare(gi, gf, oi, of, exact):
+    assert gi.shape == oi.shape
+    assert np.array_equal(gi, oi), np.argwhere(gi != oi)[:10]
+    ng, no = np.isnan(gf), np.isnan(of)
+    assert np.array_equal(ng, no)
+    if exact:
+        assert np.array_equal(gf[~ng], of[~no])
+    else:
+        x, y = gf[~ng], of[~no]
+        rel = np.abs(x - y) / np.maximum(np.maximum(np.abs(x), np.abs(y)), 1e-300)
+        assert (rel <= REL).all(), rel.max()
+
+
+def run_all(eng, arrays, mito, n_cells, n_gene_ids, n_umi_ids):
+    from sctools_amd import engine as E
+
+    dims = E.Dims(n_cells, n_gene_ids, n_umi_ids)
+    cols = E.to_device(arrays, eng.device)
+    gm = torch.from_numpy(mito).to(eng.device)
+    out = {}
+    for mode in ("cell", "gene"):
+        for fm in ("welford", "exact"):
+            gi, gf = eng.compute(cols, mode, dims, gm, gm, float_mode=fm)
+            out[(mode, fm)] = (gi.cpu().numpy(), gf.cpu().numpy())
+    ci, cf, part = eng.cell_and_gene(cols, dims, gm)
+    gi, gf = eng.finalize_partials(part)
+    out["combined_cell"] = (ci.cpu().numpy(), cf.cpu().numpy())
+    out["grouped"] = (gi.cpu().numpy(), gf.cpu().numpy())
+    return out
+
+
+@pytest.mark.parametrize("n_gene_ids,n_umi_ids,seed", [(50, 100, 1), (30_000, 1 << 20, 2)])
+def test_bucket_edge_cases_match_oracle(eng, n_gene_ids, n_umi_ids, seed):
+    arrays, mito, n_cells = craft(n_gene_ids, n_umi_ids, seed)
+    got = run_all(eng, arrays, mito, n_cells, n_gene_ids, n_umi_ids)
+    for mode in ("cell", "gene"):
+        oi, of = O.run(arrays, mode, mito, n_gene_ids, threads=8)
+        compare(*got[(mode, "welford")], oi, of, exact=True)
+        compare(*got[(mode, "exact")], oi, of, exact=False)
+        if mode == "cell":
+            compare(*got["combined_cell"], oi, of, exact=False)
+    oi, of = O.run(arrays, "gene_grouped", mito, n_gene_ids, threads=8)
+    gi, gf = got["grouped"]
+    live = oi[:, 0] > 0
+    assert np.array_equal(gi[:, 0] > 0, live)
+    compare(gi[live], gf[live], oi[live], of[live], exact=False)
+
+
+def test_global_sort_path_agrees(eng, monkeypatch):
+    arrays, mito, n_cells = craft(300, 4096, 3)
+    a = run_all(eng, arrays, mito, n_cells, 300, 4096)
+    monkeypatch.setenv("SCT_FORCE_GLOBAL_SORT", "1")
+    b = run_all(eng, arrays, mito, n_cells, 300, 4096)
+    for k in a:
+        assert np.array_equal(a[k][0], b[k][0]), k
+        assert np.array_equal(np.nan_to_num(a[k][1], nan=7.0), np.nan_to_num(b[k][1], nan=7.0)), k
