@@ -31,21 +31,30 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_HBM = 8.0e12  # MI355X HBM3E spec, MI355X_MICROARCH.md
 
-# Algorithmic HBM bytes per record per launch of each kernel (DESIGN.md §Kernels).
+# Algorithmic HBM bytes per record per launch of each kernel (DESIGN.md §3).
 ALG_BYTES = {
-    "radix_downsweep": 24,   # read key 8 + value 4, write key 8 + value 4
-    "radix_upsweep": 8,      # read key
-    "reduce_sorted": 60,     # read sorted key 8 + value 4, gather the 32-byte record, write 16-byte gene payload
-    "build_keys": 33,        # read cell/gene/umi/ref/pos (20) + bits (1), write key 8 + value 4
-    "gene_reduce": 16,       # read the 16-byte gene contribution
+    "hash_tile": 20,         # read payload w0 + w1 (16) + bucket descriptor (2), write dflags (2)
+    "bucket_scatter": 32,    # read payload 16, write payload 16 (records of the level's segments)
+    "bucket_hist": 8,        # read w0
+    "build_keys": 38,        # read cell/gene/umi/ref/pos (20) + bits/xf (2), write payload (16)
+    "stream_sums": 14,       # read entity column (4) + uy/gq/cy quality columns (10)
+    "gene_emit": 32,         # read gene/bits/xf/dflags/uy/gq (16), write 16-byte gene payload
+    "gene_reduce": 16,       # read the 16-byte gene payload
+    "radix_downsweep": 24,   # global-sort path: read key 8 + value 4, write key 8 + value 4
+    "radix_upsweep": 8,
+    "reduce_sorted": 12,
     "heads": 4,              # read the entity column
-    "welford": 10,           # read the quality columns
+    "welford": 10,
 }
 
 
-def pipeline_bytes(prof, args):
-    passes = prof.get("radix_downsweep", (0.0, 0))[1] / max(1, args.steps)
-    return 32 + 12 + 24 * passes + 44
+def pipeline_bytes(args, dims):
+    """B_alg = 32 + 12 + 24 P + 44 bytes/record, P = ceil(b / 8) LSD passes with
+    b = bits(cells per shard) + bits(gene ids) + bits(umi ids) -- a property of the workload."""
+    def bits(v):
+        return max(0, int(v - 1).bit_length())
+    b = bits(args.cells) + bits(dims.n_gene_ids) + bits(dims.n_umi_ids)
+    return 32 + 12 + 24 * ((b + 7) // 8) + 44
 
 
 def parse():
@@ -164,8 +173,8 @@ def main():
         "launches_per_step": dom_launches / args.steps,
         "alg_bytes_per_record": ALG_BYTES.get(dom_name, 0),
         # whole pipeline against SURVEY.md 8(d)'s B_alg = 32 + 12 + 24*P + 44 bytes/record
-        "pipeline_alg_bytes_per_record": pipeline_bytes(prof, args),
-        "pipeline_frac": value / world * pipeline_bytes(prof, args) / PEAK_HBM,
+        "pipeline_alg_bytes_per_record": pipeline_bytes(args, dims),
+        "pipeline_frac": value / world * pipeline_bytes(args, dims) / PEAK_HBM,
     }
     kernel_ms_per_step = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}
 

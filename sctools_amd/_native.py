@@ -10,7 +10,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsctools_gpu.so")
+LIB_PATH = os.environ.get("SCT_LIB_PATH") or os.path.join(HERE, "libsctools_gpu.so")  # override: experiments only
 
 SCT_ABI_VERSION = 1
 SCT_NI, SCT_NF, SCT_NP = 24, 12, 64

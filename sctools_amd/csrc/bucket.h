@@ -1,45 +1,64 @@
 // bucket.h -- distinct counts without a device-wide sort.
 //
-// The reference's Counters (aggregator.py:264, 300-303, 530, 595) need, per entity,
-// the records grouped by [k1 | k2 | fragment hash].  Records already arrive grouped by
-// entity (cell-sorted input, iter_tag_groups, bam.py:492-540), so only a SEGMENTED sort
-// is needed, and only far enough to make every group small:
+// The reference's Counters (aggregator.py:264, 300-303, 530, 595) need, per entity, the
+// number of distinct (k1, k2) molecule keys, (k1, k2, ref, pos, strand) fragment keys and k1
+// values, and how many of each occur exactly once.  Records already arrive grouped by entity
+// (cell-sorted input, iter_tag_groups, bam.py:492-540), so only a SEGMENTED grouping is
+// needed, and only far enough to make every group small:
 //
 //   level 0   entities of <= kBCap records are terminal buckets as they stand;
-//   level L   larger segments are split MSD-first on the next 8 key bits: a per-segment
-//             digit histogram, a scan into cursors, and a scatter that ranks each chunk
-//             in LDS and reserves one range per (chunk, digit) with a single atomic;
-//             children of <= kBCap records become terminal buckets, larger ones the next
-//             level's segments (records ping-pong between the A and B buffers);
-//   tile      one block per window of kWin record positions takes every terminal bucket
-//             that starts in the window (<= kTileCap records), sorts them in LDS on
-//             [bucket | key'] with wave-level multi-split passes over only the bits that
-//             vary in the tile, and computes the distinct-count events of reduce.h from
-//             neighbours -- every group is complete inside the tile;
-//   giant     a bucket whose whole key is fixed but still > kBCap records (one molecule
-//             with > 2047 reads at one hashed fragment) is resolved by one block.
+//   level L   larger segments are split MSD-first on the next 8 bits of key' = [k1' | k2 |
+//             fragment hash]: a per-segment digit histogram, a scan into cursors, and a
+//             scatter that ranks each chunk in LDS and reserves one range per (chunk, digit)
+//             with a single atomic; children of <= kBCap records become terminal buckets,
+//             larger ones the next level's segments (records ping-pong between buffers A, B);
+//   tile      one kWin-thread block per window of kWin record positions takes every terminal
+//             bucket that starts in the window (<= kTileCap records) and inserts each record
+//             into three LDS hash tables keyed by (bucket, k1), (bucket, k1, k2) and
+//             (molecule slot, ref, strand, pos).  The inserting record of a key is its head,
+//             the first record to find it present its "second": n_distinct = #heads and
+//             n_single = #heads - #seconds, with no sort and no neighbour scan;
+//   giant     a bucket whose whole key' is fixed but still > kBCap records (one molecule with
+//             > kBCap reads under one fragment hash) is resolved by one block.
 //
 // A k1 group or molecule split across sibling buckets (only when a single k1 value or
-// molecule has > kBCap records) carries flags so exactly one piece counts its head and
-// every piece knows the group has >= 2 records.
+// molecule has > kBCap records) carries flags so exactly one piece counts its head and the
+// group's ">= 2 records" event.
 //
-// Keys: key' = [k1' | k2 | hash] with k1' = k1 * odd mod 2^k1 (Bits::scramble), so heavy
-// genes with neighbouring ids do not pile into one top digit.  KB = k1 + k2 + h <= 40
-// leaves room for the 11-bit bucket ordinal and the 12-bit tile position in 64 bits.
+// Records travel as a 16-byte payload (two u64 words, SoA) so no pass gathers by index:
+//   w0 = key' << 24 | ref (17 bits) << 7 | strand << 6 | mapped << 5 | k1 is mitochondrial << 4
+//   w1 = record index << 32 | pos (uint32)
+// key' = [k1' | k2 | hash] with k1' = k1 * odd mod 2^k1 (Bits::scramble), so heavy genes with
+// neighbouring ids do not pile into one top digit.  KB = k1 + k2 + h <= 40.
 #pragma once
+#include <type_traits>
+
 #include "radix.h"
 #include "reduce.h"
 #include "util.h"
 
 namespace sct {
 
-constexpr int kBCap = 2047;                 // records of a terminal bucket (11-bit count)
-constexpr int kWin = 2048;                  // a tile owns the buckets starting in kWin positions
-constexpr int kTileCap = kWin + kBCap - 1;  // 4094 records per tile at most
-constexpr int kChunk = kTile;               // records per partition work item
-constexpr int kMaxKeyBits = 40;             // KB + 11 (ordinal) + 12 (position) <= 63
-static_assert(kTileCap <= kTile, "tile capacity");
+constexpr int kWin = 1024;                  // a tile owns the buckets starting in kWin positions
+constexpr int kBCap = kWin - 1;             // records of a terminal bucket
+constexpr int kTileCap = kWin + kBCap - 1;  // records per tile at most (2046)
+constexpr int kChunk = 2048;                // records per partition work item (LDS-staged)
+constexpr int kChunkItems = kChunk / kBlock;
+constexpr int kMaxKeyBits = 40;             // KB <= 40: key' sits in w0 bits [63:24]
+constexpr int kKeyShift = 24;
+constexpr int kRefBits = 17;                // mapped reference ids must be < 2^17
+constexpr uint64_t kW0Mapped = 1ull << 5;
+constexpr uint64_t kW0Mito = 1ull << 4;
+constexpr int kHBlock = 512;                // tile block: two window positions per thread
+constexpr int kHWaves = kHBlock / kWave;
+constexpr int kHTBits = 11;
+constexpr int kHTSlots = 1 << kHTBits;      // hash table slots: > kTileCap, so probing ends
+constexpr int kWinBits = 10;                // bucket ordinal (window offset) bits in the keys
+constexpr int kNarrowK1Bits = 32 - 2 - kWinBits;  // k1 ids up to 20 bits use a 32-bit k1 table
+static_assert(kTileCap < kHTSlots, "a tile's keys always fit its tables");
+static_assert(kWin == 2 * kHBlock && (1 << kWinBits) == kWin, "window layout");
 static_assert(kBCap < (1 << 11), "count field");
+static_assert(kHTSlots <= 4096, "molecule slots are 12 bits in the fragment key");
 
 // terminal bucket descriptor, stored (u16) at the bucket's first record position
 enum : uint16_t {
@@ -58,8 +77,15 @@ struct Work {
   uint32_t seg, chunk;
 };
 struct BucketCtl {  // device counters of one level (n_giant accumulates over levels)
-  uint32_t n_seg, n_work, n_giant, pad;
+  uint32_t n_seg, n_work, n_giant, err;  // err: a mapped ref id >= 2^kRefBits (set by build_keys)
 };
+
+__device__ __forceinline__ uint64_t payload_w0(uint64_t key, int32_t ref, bool reverse, bool mapped, bool mito) {
+  return (key << kKeyShift) | ((uint64_t)((uint32_t)ref & ((1u << kRefBits) - 1)) << 7) |
+         ((uint64_t)(reverse ? 1 : 0) << 6) | (mapped ? kW0Mapped : 0ull) | (mito ? kW0Mito : 0ull);
+}
+// fragment identity (ref, strand) of a payload: 18 bits
+__device__ __forceinline__ uint32_t payload_frag(uint64_t w0) { return (uint32_t)(w0 >> 6) & 0x3FFFFu; }
 
 __device__ __forceinline__ void push_segment(const Seg& sg, Seg* __restrict__ seg, Work* __restrict__ work,
                                              BucketCtl* ctl) {
@@ -72,8 +98,8 @@ __device__ __forceinline__ void push_segment(const Seg& sg, Seg* __restrict__ se
 
 // level 0: small entities are terminal buckets; larger ones become segments
 __global__ void k_bucket_level0(const int64_t* __restrict__ ent_start, int64_t n_ent, int64_t n,
-                                uint16_t* __restrict__ bdesc, Seg* __restrict__ seg, Work* __restrict__ work,
-                                BucketCtl* ctl) {
+                                uint16_t* __restrict__ bdesc, uint32_t* __restrict__ bent, Seg* __restrict__ seg,
+                                Work* __restrict__ work, BucketCtl* ctl) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n_ent) return;
   const int64_t s0 = ent_start[e];
@@ -81,6 +107,7 @@ __global__ void k_bucket_level0(const int64_t* __restrict__ ent_start, int64_t n
   const uint32_t c = (uint32_t)(s1 - s0);
   if (c <= (uint32_t)kBCap) {
     bdesc[s0] = (uint16_t)c;
+    bent[s0] = (uint32_t)e;
     return;
   }
   push_segment(Seg{(uint32_t)s0, c, (uint32_t)e, 0u}, seg, work, ctl);
@@ -105,17 +132,6 @@ __global__ void __launch_bounds__(kBlock) k_bucket_hist(const uint64_t* __restri
 #pragma unroll
   for (int w = 0; w < kWaves; w++) tot += h[w][d];
   if (tot) atomicAdd(&hist[(size_t)wk.seg * kRadix + d], tot);
-}
-
-// cursors: bucket bases of every segment (exclusive scan of its digit counts)
-__global__ void __launch_bounds__(kBlock) k_bucket_segscan(const Seg* __restrict__ seg,
-                                                           const uint32_t* __restrict__ hist,
-                                                           uint32_t* __restrict__ cur) {
-  __shared__ uint64_t lds[kWaves + 1];
-  const size_t i = (size_t)blockIdx.x * kRadix + threadIdx.x;
-  uint64_t tot;
-  const uint64_t ex = block_exclusive_scan<uint64_t>((uint64_t)hist[i], &tot, lds);
-  cur[i] = seg[blockIdx.x].start + (uint32_t)ex;
 }
 
 // Stable wave-level multi-split rank of one item: `peers` = lanes of the wave holding the
@@ -158,66 +174,68 @@ __device__ __forceinline__ uint32_t digit_starts(uint32_t (*whist)[kRadix], uint
   return run;
 }
 
-// One level's scatter: rank a chunk in LDS on the level digit, reserve one output range per
+// One level's scatter: rank a chunk in LDS on the level digit (an LDS atomic per record: the
+// order inside a child bucket is irrelevant to the hash tiles), reserve one output range per
 // present digit with one atomic on the segment's cursor, and write each digit's records as a
-// contiguous run (LDS-staged, coalesced).
+// contiguous run (LDS-staged, coalesced).  `shift` addresses w0 (key' bits + kKeyShift).
 __global__ void __launch_bounds__(kBlock) k_bucket_scatter(const uint64_t* __restrict__ kin,
-                                                           const uint32_t* __restrict__ vin,
-                                                           uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                           const uint64_t* __restrict__ vin,
+                                                           uint64_t* __restrict__ kout, uint64_t* __restrict__ vout,
                                                            const Seg* __restrict__ seg, const Work* __restrict__ work,
                                                            int shift, int bits, uint32_t* __restrict__ cur) {
-  __shared__ uint64_t s_keys[kTile];
-  __shared__ uint32_t s_vals[kTile];
-  __shared__ uint32_t s_whist[kWaves][kRadix];
-  __shared__ uint32_t s_dstart[kRadix];
+  __shared__ uint64_t s_keys[kChunk];
+  __shared__ uint64_t s_vals[kChunk];
+  __shared__ uint32_t s_cnt[kRadix];
+  __shared__ uint32_t s_start[kRadix];
   __shared__ uint32_t s_gbase[kRadix];
   __shared__ uint64_t s_scan[kWaves + 1];
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wid = threadIdx.x / kWave;
+  const int t = threadIdx.x;
   const Work wk = work[xcd_tile(blockIdx.x, gridDim.x)];
   const Seg sg = seg[wk.seg];
   const uint32_t beg = sg.start + wk.chunk * (uint32_t)kChunk;
   const int tile_n = (int)((sg.start + sg.cnt - beg) < (uint32_t)kChunk ? (sg.start + sg.cnt - beg) : kChunk);
   const uint32_t mask = (1u << bits) - 1;
-  for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_whist[0][0])[i] = 0;
+  s_cnt[t] = 0;
   __syncthreads();
-  uint64_t k[kItems];
-  uint32_t v[kItems];
-  uint16_t rank[kItems];
-  uint8_t dig[kItems];
+  uint64_t k[kChunkItems];
+  uint64_t v[kChunkItems];
+  uint32_t rk[kChunkItems];
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
-    const int q = wid * (kItems * kWave) + j * kWave + lane;
+  for (int j = 0; j < kChunkItems; j++) {
+    const int q = j * kBlock + t;
     if (q < tile_n) {
       k[j] = kin[beg + q];
       v[j] = vin[beg + q];
-    } else {
-      k[j] = ~0ull;  // padding: the top digit, ranked after every real item
-      v[j] = 0;
     }
-    const uint32_t d = (uint32_t)(k[j] >> shift) & mask;
-    dig[j] = (uint8_t)d;
-    rank[j] = (uint16_t)wlms_rank(d, bits, s_whist[wid]);
+  }
+#pragma unroll
+  for (int j = 0; j < kChunkItems; j++) {
+    const int q = j * kBlock + t;
+    if (q < tile_n) rk[j] = atomicAdd(&s_cnt[(uint32_t)(k[j] >> shift) & mask], 1u);
   }
   __syncthreads();
   {
-    uint32_t run = digit_starts(s_whist, s_dstart, s_scan);
-    const uint32_t d = threadIdx.x;
-    if (d == mask) run -= (uint32_t)(kTile - tile_n);  // padding sits at the end of the top digit
-    if (run) s_gbase[d] = atomicAdd(&cur[(size_t)wk.seg * kRadix + d], run);
+    const uint32_t c = s_cnt[t];
+    uint64_t tot;
+    const uint32_t st = (uint32_t)block_exclusive_scan<uint64_t>((uint64_t)c, &tot, s_scan);
+    s_start[t] = st;
+    if (c) s_gbase[t] = atomicAdd(&cur[(size_t)wk.seg * kRadix + t], c);
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
-    const uint32_t lp = s_whist[wid][dig[j]] + rank[j];
-    s_keys[lp] = k[j];
-    s_vals[lp] = v[j];
+  for (int j = 0; j < kChunkItems; j++) {
+    const int q = j * kBlock + t;
+    if (q < tile_n) {
+      const uint32_t lp = s_start[(uint32_t)(k[j] >> shift) & mask] + rk[j];
+      s_keys[lp] = k[j];
+      s_vals[lp] = v[j];
+    }
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < tile_n; q += kBlock) {
+  for (int q = t; q < tile_n; q += kBlock) {
     const uint64_t kk = s_keys[q];
     const uint32_t d = (uint32_t)(kk >> shift) & mask;
-    const uint32_t o = s_gbase[d] + (uint32_t)(q - (int)s_dstart[d]);
+    const uint32_t o = s_gbase[d] + (uint32_t)(q - (int)s_start[d]);
     kout[o] = kk;
     vout[o] = s_vals[q];
   }
@@ -252,433 +270,230 @@ __device__ __forceinline__ uint32_t split_flags(int Kb, int depth, int depth1, i
   return f;
 }
 
-// one block per segment, one thread per child digit
+// One block per segment, one thread per child digit: the children's record ranges (an exclusive
+// scan of the digit counts; the scatter's cursors) and their classification -- terminal
+// bucket, giant, or next-level segment.  The block's new segments and work items are reserved
+// with one atomic each.
 __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restrict__ seg,
                                                             const uint32_t* __restrict__ hist,
-                                                            const uint32_t* __restrict__ cur, int depth, int bits,
+                                                            uint32_t* __restrict__ cur, int depth, int bits,
                                                             int K1, int KM, int KB, int parity,
-                                                            uint16_t* __restrict__ bdesc, Seg* __restrict__ nseg,
-                                                            Work* __restrict__ nwork, Seg* __restrict__ giants,
-                                                            BucketCtl* ctl) {
+                                                            uint16_t* __restrict__ bdesc, uint32_t* __restrict__ bent,
+                                                            Seg* __restrict__ nseg, Work* __restrict__ nwork,
+                                                            Seg* __restrict__ giants, BucketCtl* ctl) {
   __shared__ uint32_t s_c[kRadix];
+  __shared__ uint64_t s_scan[kWaves + 1];
+  __shared__ uint32_t s_base[2];
   const int d = threadIdx.x;
   const size_t i = (size_t)blockIdx.x * kRadix + d;
   const Seg sg = seg[blockIdx.x];
   const uint32_t c = hist[i];
   s_c[d] = c;
-  __syncthreads();
-  if (c == 0) return;
-  const uint32_t start = cur[i] - c;
+  uint64_t tot_c;
+  const uint32_t start = sg.start + (uint32_t)block_exclusive_scan<uint64_t>((uint64_t)c, &tot_c, s_scan);
+  cur[i] = start;
   const int depth1 = depth + bits;
-  uint32_t fl = split_flags(K1, depth, depth1, d, sg.flags, s_c, BD_K1_NOHEAD, BD_K1_MULTI);
-  fl |= split_flags(KM, depth, depth1, d, sg.flags, s_c, BD_MOL_NOHEAD, BD_MOL_MULTI);
+  uint32_t fl = 0;
+  if (c) {
+    fl = split_flags(K1, depth, depth1, d, sg.flags, s_c, BD_K1_NOHEAD, BD_K1_MULTI);
+    fl |= split_flags(KM, depth, depth1, d, sg.flags, s_c, BD_MOL_NOHEAD, BD_MOL_MULTI);
+  }
   const uint32_t par = parity ? BD_PARITY : 0u;
-  if (c <= (uint32_t)kBCap) {
+  const bool terminal = c && c <= (uint32_t)kBCap;
+  const bool giant = c > (uint32_t)kBCap && depth1 >= KB;
+  const bool push = c > (uint32_t)kBCap && !giant;
+  if (terminal) {
     bdesc[start] = (uint16_t)(c | fl | par);
-  } else if (depth1 >= KB) {
+    bent[start] = sg.ent;
+  } else if (giant) {
     const uint32_t id = atomicAdd(&ctl->n_giant, 1u);
     giants[id] = Seg{start, c, sg.ent, fl | par};
-  } else {
-    push_segment(Seg{start, c, sg.ent, fl}, nseg, nwork, ctl);
   }
-}
-
-__device__ __forceinline__ uint32_t entity_of(const int64_t* __restrict__ ent_start, int64_t n_ent, int64_t pos) {
-  int64_t lo = 0, hi = n_ent - 1;  // largest e with ent_start[e] <= pos
-  while (lo < hi) {
-    const int64_t mid = (lo + hi + 1) >> 1;
-    if (ent_start[mid] <= pos)
-      lo = mid;
-    else
-      hi = mid - 1;
+  const uint32_t nw = push ? (c + kChunk - 1) / kChunk : 0u;
+  uint64_t tot_s, tot_w;
+  const uint32_t so = (uint32_t)block_exclusive_scan<uint64_t>(push ? 1 : 0, &tot_s, s_scan);
+  const uint32_t wo = (uint32_t)block_exclusive_scan<uint64_t>(nw, &tot_w, s_scan);
+  if (d == 0 && tot_s) {
+    s_base[0] = atomicAdd(&ctl->n_seg, (uint32_t)tot_s);
+    s_base[1] = atomicAdd(&ctl->n_work, (uint32_t)tot_w);
   }
-  return (uint32_t)lo;
-}
-
-// first entity of every window: entity of record position w * kWin (w = 0..n_win; entry n_win is
-// the entity of the last record).  Tiles then search only their own slice of ent_start.
-__global__ void k_window_entities(const int64_t* __restrict__ ent_start, int64_t n_ent, int64_t n, int64_t n_win,
-                                  uint32_t* __restrict__ win_ent) {
-  const int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (w > n_win) return;
-  const int64_t p = w * kWin < n ? w * kWin : n - 1;
-  win_ent[w] = entity_of(ent_start, n_ent, p);
-}
-
-// exclusive max-scan over the block (values >= 0); lds needs kWaves entries; barriers inside
-__device__ __forceinline__ uint32_t block_exclusive_max(uint32_t v, uint32_t* lds) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wid = threadIdx.x / kWave;
-  uint32_t x = v;
-  for (int off = 1; off < kWave; off <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, off);
-    if (lane >= off) x = y > x ? y : x;
-  }
-  if (lane == kWave - 1) lds[wid] = x;
   __syncthreads();
-  uint32_t carry = 0;
-  for (int w = 0; w < wid; w++) carry = lds[w] > carry ? lds[w] : carry;
-  uint32_t ex = (uint32_t)__shfl_up((int)x, 1);
-  if (lane == 0) ex = 0;
-  __syncthreads();
-  return ex > carry ? ex : carry;
+  if (push) {
+    const uint32_t id = s_base[0] + so;
+    nseg[id] = Seg{start, c, sg.ent, fl};
+    for (uint32_t k = 0; k < nw; k++) nwork[s_base[1] + wo + k] = Work{id, k};
+  }
 }
 
-template <bool kCell, bool kGene>
-__global__ void __launch_bounds__(kBlock) k_bucket_tile(const uint16_t* __restrict__ bdesc,
-                                                        const uint64_t* __restrict__ keys_a,
-                                                        const uint32_t* __restrict__ vals_a,
-                                                        const uint64_t* __restrict__ keys_b,
-                                                        const uint32_t* __restrict__ vals_b, int64_t n,
-                                                        const int64_t* __restrict__ ent_start,
-                                                        const uint32_t* __restrict__ win_ent, RecCols r,
-                                                        const uint8_t* __restrict__ k1_is_mito, Bits b,
-                                                        int64_t* __restrict__ partials,
-                                                        uint16_t* __restrict__ dflags) {
-  __shared__ uint64_t s_x[kTile];     // sort keys [bucket | key' | tile position]; scratch before the sort
-  __shared__ uint32_t s_val[kTile];   // values by tile position
-  __shared__ uint32_t s_bpos[kWin];   // bucket start (record position)
-  __shared__ uint16_t s_boff[kWin + 1];
-  __shared__ uint16_t s_bd[kWin];
-  __shared__ uint32_t s_bent[kWin];
-  __shared__ uint32_t s_whist[kWaves][kRadix];
-  __shared__ uint64_t s_scan[kWaves + 1];
-  __shared__ uint64_t s_red[2][kWaves];
-  __shared__ uint32_t s_edge[4][kWaves];
-  uint32_t* s_es = reinterpret_cast<uint32_t*>(s_x);                  // entity starts of the window
-  uint16_t* s_bid = reinterpret_cast<uint16_t*>(s_x) + 2 * (kWin + 8);  // bucket of each tile position
-  constexpr int kPer = kWin / kBlock;
+// ---- LDS hash tables: entries key << 2 | state, state bit 0 = present, bit 1 = seen twice ----
+__device__ __forceinline__ uint32_t ht_home(unsigned long long key) {
+  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - kHTBits));
+}
+__device__ __forceinline__ uint32_t ht_home(unsigned int key) { return (key * 0x9E3779B1u) >> (32 - kHTBits); }
+
+// Insert `key` (low two bits zero).  Returns the key's slot; ev = 1 for the record that inserted
+// the key (its head), 2 for the first record that found it present, else 0.  The table has
+// more slots than a tile has records, so the probe always ends.
+template <typename E>
+__device__ __forceinline__ uint32_t ht_insert(E* T, E key, int& ev) {
+  uint32_t h = ht_home(key);
+  while (true) {
+    const E old = atomicCAS(&T[h], (E)0, (E)(key | 1));
+    if (old == 0) {
+      ev = 1;
+      return h;
+    }
+    if ((old & ~(E)3) == key) {
+      ev = 0;
+      if (!(old & 2) && !(atomicOr(&T[h], (E)2) & 2)) ev = 2;
+      return h;
+    }
+    h = (h + 1) & (kHTSlots - 1);
+  }
+}
+
+// kWideK1: k1 ids need more than kNarrowK1Bits bits (64-bit k1 table entries)
+template <bool kCell, bool kGene, bool kWideK1>
+__global__ void __launch_bounds__(kHBlock) k_hash_tile(const uint16_t* __restrict__ bdesc,
+                                                       const uint32_t* __restrict__ bent,
+                                                       const uint64_t* __restrict__ w0_a,
+                                                       const uint64_t* __restrict__ w1_a,
+                                                       const uint64_t* __restrict__ w0_b,
+                                                       const uint64_t* __restrict__ w1_b, int64_t n, Bits b,
+                                                       int64_t* __restrict__ partials,
+                                                       uint16_t* __restrict__ dflags) {
+  using K1E = typename std::conditional<kWideK1, unsigned long long, unsigned int>::type;
+  __shared__ K1E s_k1[kHTSlots];                  // (bucket, k1)
+  __shared__ unsigned long long s_mol[kHTSlots];  // (bucket, k1, k2)
+  __shared__ unsigned long long s_frg[kHTSlots];  // (molecule slot, ref, strand, pos)
+  __shared__ uint16_t s_bd[kWin];                 // descriptor of the bucket starting at window offset x
+  __shared__ uint32_t s_bent[kWin];               // its entity
+  __shared__ uint32_t s_red[kHWaves];
+  __shared__ int s_last;
   const int t = threadIdx.x;
-  const int lane = t & (kWave - 1);
-  const int wid = t / kWave;
   const unsigned wb = xcd_tile(blockIdx.x, gridDim.x);
   const int64_t w0 = (int64_t)wb * kWin;
   const int win_n = (int)((n - w0) < kWin ? (n - w0) : kWin);
-
-  // 1. bucket starts in the window, in position order
-  uint16_t dsc[kPer];
-  uint32_t nv = 0;
+  // descriptors of window offsets 2t, 2t+1 (independent loads); tables cleared meanwhile
+  const int p0 = 2 * t;
+  uint16_t dsc[2];
+  uint32_t ent[2];
 #pragma unroll
-  for (int j = 0; j < kPer; j++) {
-    const int q = t * kPer + j;
-    dsc[j] = q < win_n ? bdesc[w0 + q] : (uint16_t)0;
-    nv += dsc[j] != 0;
+  for (int i = 0; i < 2; i++) {
+    dsc[i] = p0 + i < win_n ? bdesc[w0 + p0 + i] : (uint16_t)0;
+    ent[i] = dsc[i] ? bent[w0 + p0 + i] : 0u;
   }
-  uint64_t tot;
-  uint32_t bi = (uint32_t)block_exclusive_scan<uint64_t>(nv, &tot, s_scan);
-  const int nb = (int)tot;
-#pragma unroll
-  for (int j = 0; j < kPer; j++) {
-    if (dsc[j]) {
-      s_bpos[bi] = (uint32_t)(w0 + t * kPer + j);
-      s_bd[bi] = dsc[j];
-      bi++;
-    }
-  }
-  __syncthreads();
-  // 2. tile offsets of the buckets; the window's slice of entity starts
-  uint32_t cnt[kPer];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int j = 0; j < kPer; j++) {
-    const int x = t * kPer + j;
-    cnt[j] = x < nb ? (uint32_t)(s_bd[x] & BD_COUNT) : 0u;
-    sum += cnt[j];
-  }
-  uint32_t off = (uint32_t)block_exclusive_scan<uint64_t>(sum, &tot, s_scan);
-  const int tn = (int)tot;
-#pragma unroll
-  for (int j = 0; j < kPer; j++) {
-    const int x = t * kPer + j;
-    if (x < nb) s_boff[x] = (uint16_t)off;
-    off += cnt[j];
-  }
-  if (t == 0) s_boff[nb] = (uint16_t)tn;
-  const uint32_t e_lo = win_ent[wb];
-  const int ne = (int)(win_ent[wb + 1] - e_lo) + 1;  // <= kWin + 1
-  for (int x = t; x < ne; x += kBlock) s_es[x] = (uint32_t)ent_start[e_lo + x];
-  for (int q = t; q < tn; q += kBlock) s_bid[q] = 0;
-  __syncthreads();
-  if (tn == 0) return;  // block-uniform
-  for (int x = t; x < nb; x += kBlock) {
-    s_bid[s_boff[x]] = (uint16_t)x;  // bucket start marker
-    const uint32_t pos = s_bpos[x];
-    int lo = 0, hi = ne - 1;  // entity: largest slice index with start <= pos
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_es[mid] <= pos)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    s_bent[x] = e_lo + (uint32_t)lo;
-  }
-  __syncthreads();
-  {  // fill: bucket id of every tile position = running max of the start markers
-    uint32_t run = 0;
-#pragma unroll
-    for (int j = 0; j < kItems; j++) {
-      const int q = t * kItems + j;
-      if (q < tn) run = s_bid[q] > run ? s_bid[q] : run;
-    }
-    uint32_t m = block_exclusive_max(run, &s_whist[0][0]);
-#pragma unroll
-    for (int j = 0; j < kItems; j++) {
-      const int q = t * kItems + j;
-      if (q < tn) {
-        m = s_bid[q] > m ? s_bid[q] : m;
-        s_bid[q] = (uint16_t)m;
-      }
-    }
-  }
-  __syncthreads();
-
-  // 3. load the records in the wave-major item layout (wave w owns positions [w*per, (w+1)*per))
-  const int KB = b.k1 + b.k2 + b.h;
-  const int per = ((tn + kBlock - 1) / kBlock) * kWave;  // items per wave, a multiple of 64
-  const int rounds = per / kWave;
-  const uint64_t kbm = (1ull << KB) - 1;
-  uint64_t k[kItems];
-  uint64_t vor = 0, vand = ~0ull;
-#pragma unroll
-  for (int j = 0; j < kItems; j++) {
-    k[j] = ~0ull;
-    if (j < rounds) {
-      const int q = wid * per + j * kWave + lane;
-      if (q < tn) {
-        const int bk = s_bid[q];
-        const uint32_t gp = s_bpos[bk] + (uint32_t)(q - (int)s_boff[bk]);
-        const bool pb = s_bd[bk] & BD_PARITY;
-        // ids >= the dictionary sizes must not reach the ordinal bits
-        const uint64_t kk = (pb ? keys_b[gp] : keys_a[gp]) & kbm;
-        s_val[q] = pb ? vals_b[gp] : vals_a[gp];
-        k[j] = ((uint64_t)bk << (KB + 12)) | (kk << 12) | (uint64_t)q;
-        vor |= k[j];
-        vand &= k[j];
-      }
-    }
-  }
-  // bits that vary across the tile: only those need sorting
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    vor |= __shfl_xor(vor, o);
-    vand &= __shfl_xor(vand, o);
-  }
-  if (lane == 0) {
-    s_red[0][wid] = vor;
-    s_red[1][wid] = vand;
-  }
-  __syncthreads();
-  uint64_t vary = 0;
   {
-    uint64_t o = 0, a = ~0ull;
-#pragma unroll
-    for (int w = 0; w < kWaves; w++) {
-      o |= s_red[0][w];
-      a &= s_red[1][w];
-    }
-    vary = (o ^ a) >> 12 << 12;
+    uint4* z = reinterpret_cast<uint4*>(s_mol);
+    for (int i = t; i < kHTSlots / 2; i += kHBlock) z[i] = make_uint4(0, 0, 0, 0);
+    z = reinterpret_cast<uint4*>(s_frg);
+    for (int i = t; i < kHTSlots / 2; i += kHBlock) z[i] = make_uint4(0, 0, 0, 0);
+    z = reinterpret_cast<uint4*>(s_k1);
+    for (int i = t; i < (int)(kHTSlots * sizeof(K1E) / 16); i += kHBlock) z[i] = make_uint4(0, 0, 0, 0);
   }
-  const int hb = vary ? 63 - __builtin_clzll(vary) : -1;
-
-  // 4. LSD passes in LDS over bits [12, hb]; items stay in registers between passes
-  for (int shift = 12; shift <= hb; shift += kRadixBits) {
-    const int nbits = (hb + 1 - shift) < kRadixBits ? (hb + 1 - shift) : kRadixBits;
-    const uint32_t mask = (1u << nbits) - 1;
-    for (int i = t; i < kWaves * kRadix; i += kBlock) (&s_whist[0][0])[i] = 0;
-    __syncthreads();
-    uint16_t rank[kItems];
-    uint8_t dig[kItems];
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
-      if (j < rounds) {
-        const uint32_t d = (uint32_t)(k[j] >> shift) & mask;
-        dig[j] = (uint8_t)d;
-        rank[j] = (uint16_t)wlms_rank(d, nbits, s_whist[wid]);
-      }
-    }
-    __syncthreads();
-    digit_starts(s_whist, nullptr, s_scan);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kItems; j++)
-      if (j < rounds) s_x[s_whist[wid][dig[j]] + rank[j]] = k[j];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kItems; j++)
-      if (j < rounds) k[j] = s_x[wid * per + j * kWave + lane];
-    __syncthreads();
+  for (int i = 0; i < 2; i++) {
+    s_bd[p0 + i] = dsc[i];
+    s_bent[p0 + i] = ent[i];
   }
-  if (hb < 12) {  // already in order (one key' value): place the items by position
-#pragma unroll
-    for (int j = 0; j < kItems; j++)
-      if (j < rounds) {
-        const int q = wid * per + j * kWave + lane;
-        if (q < tn) s_x[q] = k[j];
-      }
-    __syncthreads();
-  }
-
-  // 5. distinct-count events from sorted neighbours (reduce.h semantics + split flags).
-  // Blocked: thread t owns sorted positions [16t, 16t + 16).  Records whose fragment key
-  // equals a neighbour's gather (ref, strand, pos) all at once; the neighbour of the first /
-  // last item comes from the adjacent lane or, at a wave edge, through LDS.
-  const int q0 = t * kItems;
-  uint32_t fr[kItems], fp[kItems];  // fragment identity: ref * 2 + strand, pos (~0: none)
-  uint8_t fl[kItems];               // 1: equal key before, 2: equal key after, 4: mapped
-#pragma unroll
-  for (int j = 0; j < kItems; j++) {
-    const int q = q0 + j;
-    fr[j] = ~0u;
-    fp[j] = ~0u;
-    fl[j] = 0;
-    if (q < tn) {
-      const uint64_t sk = s_x[q];
-      const uint64_t fk = sk >> 12;
-      const uint32_t v = s_val[sk & 0xFFF];
-      const bool mapped = !(v & kUnmappedValBit);
-      const bool ep = q > 0 && (s_x[q - 1] >> 12) == fk;
-      const bool en = q + 1 < tn && (s_x[q + 1] >> 12) == fk;
-      fl[j] = (ep ? 1 : 0) | (en ? 2 : 0) | (mapped ? 4 : 0);
-      if (mapped && (ep || en)) {
-        const uint32_t i = v & ~kUnmappedValBit;
-        fr[j] = (uint32_t)r.ref[i] * 2u + ((r.bits[i] & SCT_B_REVERSE) ? 1u : 0u);
-        fp[j] = (uint32_t)r.pos[i];
-      }
-    }
-  }
-  uint32_t pfr = (uint32_t)__shfl_up((int)fr[kItems - 1], 1), pfp = (uint32_t)__shfl_up((int)fp[kItems - 1], 1);
-  uint32_t nfr = (uint32_t)__shfl_down((int)fr[0], 1), nfp = (uint32_t)__shfl_down((int)fp[0], 1);
-  if (lane == kWave - 1) {
-    s_edge[0][wid] = fr[kItems - 1];
-    s_edge[1][wid] = fp[kItems - 1];
-  }
-  if (lane == 0) {
-    s_edge[2][wid] = fr[0];
-    s_edge[3][wid] = fp[0];
-  }
+  // bucket of window offset x: the last start at or before x (max-scan of x + 1 markers)
+  const uint32_t m0 = dsc[0] ? (uint32_t)p0 + 1 : 0u;
+  const uint32_t m1 = dsc[1] ? (uint32_t)p0 + 2 : (m0);
+  const uint32_t ex = block_exclusive_max_n<kHBlock>(m1, s_red);  // has barriers
+  uint32_t inc[2];
+  inc[0] = m0 > ex ? m0 : ex;
+  inc[1] = m1 > inc[0] ? m1 : inc[0];
+  if (t == kHBlock - 1) s_last = (int)inc[1] - 1;
   __syncthreads();
-  if (lane == 0 && wid > 0) {
-    pfr = s_edge[0][wid - 1];
-    pfp = s_edge[1][wid - 1];
-  }
-  if (lane == kWave - 1 && wid < kWaves - 1) {
-    nfr = s_edge[2][wid + 1];
-    nfp = s_edge[3][wid + 1];
-  }
+  const int last = s_last;
+  if (last < 0) return;  // block-uniform: no bucket starts in this window
+  const int end_off = last + (int)(s_bd[last] & BD_COUNT);  // the last bucket may run past the window
 
-  const int sh1 = 12 + b.k2 + b.h;
-  const int shm = 12 + b.h;
-  const uint32_t k1m = b.k1_mask();
-  int64_t acc[kDistinct];
+  const int KB = b.k1 + b.k2 + b.h;
+  const uint64_t kmask = (1ull << KB) - 1;
+  const int sh_mol = b.h, sh_k1 = b.k2 + b.h;
+  const int mol_bits = b.k1 + b.k2;
+  int32_t acc[kDistinct];
 #pragma unroll
   for (int i = 0; i < kDistinct; i++) acc[i] = 0;
   int64_t cur_e = -1;
   const auto slot = [](int i) { return distinct_slot(i); };
+  // items 0, 1: window offsets 2t, 2t+1; items 2, 3: overflow offsets kWin + 2t, kWin + 2t + 1
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
-    const int q = q0 + j;
-    const bool valid = q < tn;
-    const uint64_t sk = valid ? s_x[q] : 0ull;
-    const int bk = (int)(sk >> (KB + 12));
-    const int64_t e = valid ? (int64_t)s_bent[bk] : cur_e;
+  for (int j = 0; j < 4; j++) {
+    const int q = (j < 2 ? 0 : kWin) + p0 + (j & 1);  // offset from w0
+    const int bs = j < 2 ? (int)inc[j] - 1 : last;    // the bucket's start offset = its ordinal
+    // inside the bucket's extent (a giant's range has no descriptor and follows some bucket)
+    const bool valid = j < 2 ? (bs >= 0 && q < win_n && q < bs + (int)(s_bd[bs] & BD_COUNT)) : (q < end_off);
+    const int64_t e = valid ? (int64_t)s_bent[bs] : cur_e;
     wave_flush<kDistinct>(acc, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
     if (!valid) continue;
     cur_e = e;
-    const uint64_t prev = q > 0 ? s_x[q - 1] : ~0ull;
-    const uint64_t next = q + 1 < tn ? s_x[q + 1] : ~0ull;
-    const uint32_t bd = s_bd[bk];
-    const bool k1_head = (prev >> sh1) != (sk >> sh1) && !(bd & BD_K1_NOHEAD);
-    const bool k1_multi = k1_head && ((bd & BD_K1_MULTI) || (next >> sh1) == (sk >> sh1));
-    const bool mol_head = (prev >> shm) != (sk >> shm) && !(bd & BD_MOL_NOHEAD);
-    const bool mol_single = mol_head && !(bd & BD_MOL_MULTI) && (next >> shm) != (sk >> shm);
-    const uint32_t v = s_val[sk & 0xFFF];
-    const uint32_t i = v & ~kUnmappedValBit;
-    uint16_t f = (mol_head ? DF_MOL_HEAD : 0) | (mol_single ? DF_MOL_SINGLE : 0) | (k1_head ? DF_K1_HEAD : 0) |
-                 (k1_multi ? DF_K1_MULTI : 0);
+    const uint32_t bd = s_bd[bs];
+    const bool pb = bd & BD_PARITY;
+    const uint64_t x0 = pb ? w0_b[w0 + q] : w0_a[w0 + q];
+    const uint64_t x1 = pb ? w1_b[w0 + q] : w1_a[w0 + q];
+    const uint64_t key = (x0 >> kKeyShift) & kmask;  // ids >= the dictionary sizes stay inside KB bits
+    int ek, em, ef = 0;
+    ht_insert<K1E>(s_k1, (K1E)((((uint64_t)bs << b.k1) | (key >> sh_k1)) << 2), ek);
+    const uint32_t ms =
+        ht_insert<unsigned long long>(s_mol, (((uint64_t)bs << mol_bits) | (key >> sh_mol)) << 2, em);
+    if (x0 & kW0Mapped) {
+      const uint64_t fk = ((((uint64_t)ms << 18) | payload_frag(x0)) << 32) | (uint32_t)x1;
+      ht_insert<unsigned long long>(s_frg, fk << 2, ef);
+    }
+    // split groups: only the first piece counts the head, and it also carries the multi event
+    const bool k1_head = ek == 1 && !(bd & BD_K1_NOHEAD);
+    const bool k1_multi = (bd & BD_K1_MULTI) ? k1_head : ek == 2;
+    const bool mol_head = em == 1 && !(bd & BD_MOL_NOHEAD);
+    const bool mol_second = (bd & BD_MOL_MULTI) ? mol_head : em == 2;
     acc[0] += mol_head;
-    acc[1] += mol_single;
+    acc[1] += (int32_t)mol_head - (int32_t)mol_second;
+    acc[2] += ef == 1;
+    acc[3] += (int32_t)(ef == 1) - (int32_t)(ef == 2);
     acc[4] += k1_head;
     acc[5] += k1_multi;
-    if constexpr (kCell) {
-      if (k1_head) acc[6] += k1_is_mito[b.unscramble((uint32_t)(sk >> sh1) & k1m)];
+    if constexpr (kCell) acc[6] += (k1_head && (x0 & kW0Mito)) ? 1 : 0;
+    if constexpr (kGene) {
+      const uint16_t f = (mol_head ? (DF_MOL_HEAD | DF_MOL_SINGLE) : 0) | (mol_second ? DF_MOL_SECOND : 0) |
+                         (ef == 1 ? (DF_FRAG_FIRST | DF_FRAG_SINGLE) : 0) | (ef == 2 ? DF_FRAG_SECOND : 0) |
+                         (k1_head ? DF_K1_HEAD : 0) | (k1_multi ? DF_K1_MULTI : 0);
+      dflags[x1 >> 32] = f;
     }
-    if (fl[j] & 4) {
-      const uint32_t pr = j > 0 ? fr[j - 1] : pfr, pp = j > 0 ? fp[j - 1] : pfp;
-      const uint32_t nr = j + 1 < kItems ? fr[j + 1] : nfr, np = j + 1 < kItems ? fp[j + 1] : nfp;
-      const uint64_t fk = sk >> 12;
-      bool is_first = true, single = true;
-      if (fl[j] & 1) {
-        if (pr == fr[j] && pp == fp[j]) {
-          is_first = false;
-        } else {  // the neighbour holds another fragment under the same hash: scan the sub-run
-          for (int pq = q - 2; pq >= 0; pq--) {
-            const uint64_t kq = s_x[pq];
-            if ((kq >> 12) != fk) break;
-            const uint32_t vq = s_val[kq & 0xFFF];
-            if (!(vq & kUnmappedValBit) && same_fragment(r, vq, i)) {
-              is_first = false;
-              break;
-            }
-          }
-        }
-      }
-      if (is_first && (fl[j] & 2)) {
-        if (nr == fr[j] && np == fp[j]) {
-          single = false;
-        } else {
-          for (int pq = q + 2; pq < tn; pq++) {
-            const uint64_t kq = s_x[pq];
-            if ((kq >> 12) != fk) break;
-            const uint32_t vq = s_val[kq & 0xFFF];
-            if (!(vq & kUnmappedValBit) && same_fragment(r, vq, i)) {
-              single = false;
-              break;
-            }
-          }
-        }
-      }
-      if (is_first) {
-        acc[2] += 1;
-        acc[3] += single;
-        f |= DF_FRAG_FIRST | (single ? DF_FRAG_SINGLE : 0);
-      }
-    }
-    if constexpr (kGene) dflags[i] = f;
   }
   wave_flush<kDistinct>(acc, cur_e >= 0, cur_e, partials, slot);
 }
 
 // A bucket whose whole key' is fixed and still holds > kBCap records: one piece of one
 // molecule at one fragment hash.  One block; fragments resolved exactly by repeatedly taking
-// the first unassigned mapped record as a representative.  `mark` is the other buffer's
-// value array over the same range (dead: the parent segment was scattered out of it).
+// the first unassigned mapped record as a representative.  `mark` is the other buffer's w1
+// array over the same range (dead: the parent segment was scattered out of it).
 template <bool kCell, bool kGene>
 __global__ void __launch_bounds__(kBlock) k_bucket_giant(const Seg* __restrict__ giants,
-                                                         const uint64_t* __restrict__ keys_a,
-                                                         uint32_t* __restrict__ vals_a,
-                                                         const uint64_t* __restrict__ keys_b,
-                                                         uint32_t* __restrict__ vals_b, RecCols r,
-                                                         const uint8_t* __restrict__ k1_is_mito, Bits b,
+                                                         const uint64_t* __restrict__ w0_a,
+                                                         uint64_t* __restrict__ w1_a,
+                                                         const uint64_t* __restrict__ w0_b,
+                                                         uint64_t* __restrict__ w1_b,
                                                          int64_t* __restrict__ partials,
                                                          uint16_t* __restrict__ dflags) {
   __shared__ uint64_t s_red[kWaves];
   __shared__ uint32_t s_min[kWaves];
   const Seg g = giants[blockIdx.x];
   const bool pb = g.flags & BD_PARITY;
-  const uint32_t* vals = pb ? vals_b : vals_a;
-  uint32_t* mark = pb ? vals_a : vals_b;
+  const uint64_t* w0 = pb ? w0_b : w0_a;
+  const uint64_t* w1 = pb ? w1_b : w1_a;
+  uint64_t* mark = pb ? w1_a : w1_b;
   const int t = threadIdx.x;
   const int lane = t & (kWave - 1);
   const int wid = t / kWave;
   const bool k1_head = !(g.flags & BD_K1_NOHEAD);
   const bool mol_head = !(g.flags & BD_MOL_NOHEAD);
   for (uint32_t p = t; p < g.cnt; p += kBlock) {
-    const uint32_t v = vals[g.start + p];
-    mark[g.start + p] = (v & kUnmappedValBit) ? 1u : 0u;
+    mark[g.start + p] = (w0[g.start + p] & kW0Mapped) ? 0ull : 1ull;
     if constexpr (kGene) {
       uint16_t f = 0;
       if (p == 0) f = (k1_head ? (DF_K1_HEAD | DF_K1_MULTI) : 0) | (mol_head ? DF_MOL_HEAD : 0);
-      dflags[v & ~kUnmappedValBit] = f;
+      dflags[w1[g.start + p] >> 32] = f;
     }
   }
   __syncthreads();
@@ -701,13 +516,13 @@ __global__ void __launch_bounds__(kBlock) k_bucket_giant(const Seg* __restrict__
     for (int w = 0; w < kWaves; w++) rep = s_min[w] < rep ? s_min[w] : rep;
     __syncthreads();
     if (rep == 0xFFFFFFFFu) break;  // block-uniform
-    const uint32_t ir = vals[g.start + rep] & ~kUnmappedValBit;
+    const uint32_t fr = payload_frag(w0[g.start + rep]);
+    const uint32_t fp = (uint32_t)w1[g.start + rep];
     uint64_t c = 0;
     for (uint32_t p = rep + t; p < g.cnt; p += kBlock) {
       if (mark[g.start + p]) continue;
-      const uint32_t ip = vals[g.start + p] & ~kUnmappedValBit;
-      if (same_fragment(r, ip, ir)) {
-        mark[g.start + p] = 1u;
+      if (payload_frag(w0[g.start + p]) == fr && (uint32_t)w1[g.start + p] == fp) {
+        mark[g.start + p] = 1ull;
         c++;
       }
     }
@@ -719,15 +534,14 @@ __global__ void __launch_bounds__(kBlock) k_bucket_giant(const Seg* __restrict__
     for (int w = 0; w < kWaves; w++) tot += s_red[w];
     n_frag += 1;
     n_single += tot == 1;
-    if (kGene && t == 0) dflags[ir] |= DF_FRAG_FIRST | (tot == 1 ? DF_FRAG_SINGLE : 0);
+    if (kGene && t == 0) dflags[w1[g.start + rep] >> 32] |= DF_FRAG_FIRST | (tot == 1 ? DF_FRAG_SINGLE : 0);
     __syncthreads();
   }
   if (t == 0) {
     int64_t* row = partials + (int64_t)g.ent * SCT_NP;
-    const uint64_t key = (pb ? keys_b : keys_a)[g.start];
-    const uint32_t k1 = b.unscramble((uint32_t)(key >> (b.k2 + b.h)) & b.k1_mask());
+    const bool mito = w0[g.start] & kW0Mito;
     const int64_t add[kDistinct] = {mol_head ? 1 : 0, 0, n_frag, n_single, k1_head ? 1 : 0, k1_head ? 1 : 0,
-                                    (kCell && k1_head) ? (int64_t)k1_is_mito[k1] : 0};
+                                    (kCell && k1_head && mito) ? 1 : 0};
     for (int i = 0; i < kDistinct; i++)
       if (add[i]) atomicAdd((unsigned long long*)&row[distinct_slot(i)], (unsigned long long)add[i]);
   }

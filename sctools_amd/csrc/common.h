@@ -72,8 +72,10 @@ enum : uint32_t {
   GF_FRAG_SINGLE = 1u << 11,
   GF_CG_HEAD = 1u << 12,   // first record of a (cell, gene) pair -> number_cells_expressing
   GF_CG_MULTI = 1u << 13,  // ... of a pair with > 1 record -> number_cells_detected_multiple
+  GF_MOL_SECOND = 1u << 14,   // -1 on molecules_with_single_read_evidence (reduce.h DF_MOL_SECOND)
+  GF_FRAG_SECOND = 1u << 15,  // -1 on fragments_with_single_read_evidence
 };
-constexpr int kGeneFlags = 14;
+constexpr int kGeneFlags = 14;  // lanes: the two SECOND bits subtract from the SINGLE lanes
 
 struct __attribute__((aligned(16))) GenePayload {
   uint32_t gene;

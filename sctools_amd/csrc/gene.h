@@ -50,7 +50,8 @@ __global__ void __launch_bounds__(kBlock) k_gene_emit(const int32_t* __restrict_
     }
     f |= (df & DF_MOL_HEAD ? GF_MOL_HEAD : 0) | (df & DF_MOL_SINGLE ? GF_MOL_SINGLE : 0) |
          (df & DF_FRAG_FIRST ? GF_FRAG_FIRST : 0) | (df & DF_FRAG_SINGLE ? GF_FRAG_SINGLE : 0) |
-         (df & DF_K1_HEAD ? GF_CG_HEAD : 0) | (df & DF_K1_MULTI ? GF_CG_MULTI : 0);
+         (df & DF_K1_HEAD ? GF_CG_HEAD : 0) | (df & DF_K1_MULTI ? GF_CG_MULTI : 0) |
+         (df & DF_MOL_SECOND ? GF_MOL_SECOND : 0) | (df & DF_FRAG_SECOND ? GF_FRAG_SECOND : 0);
     GenePayload gp;
     gp.gene = g;
     gp.flags = (uint16_t)f;
@@ -105,7 +106,7 @@ struct GeneAcc {
   __device__ __forceinline__ void flush(unsigned long long* bin) const {
 #pragma unroll
     for (int i = 0; i < 1 + kGeneFlags; i++)
-      if (c[i]) atomicAdd(&bin[i], (unsigned long long)c[i]);
+      if (c[i]) atomicAdd(&bin[i], (unsigned long long)(int64_t)c[i]);  // may be negative
 #pragma unroll
     for (int i = 0; i < 3 * kStreamLanes; i++)
       if (l[i]) atomicAdd(&bin[1 + kGeneFlags + i], (unsigned long long)l[i]);
@@ -145,6 +146,8 @@ __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __res
       acc.c[0] += 1;
 #pragma unroll
       for (int f = 0; f < kGeneFlags; f++) acc.c[1 + f] += (g.flags >> f) & 1u;
+      acc.c[1 + 9] -= (g.flags >> 14) & 1u;   // GF_MOL_SECOND on the GF_MOL_SINGLE lane
+      acc.c[1 + 11] -= (g.flags >> 15) & 1u;  // GF_FRAG_SECOND on the GF_FRAG_SINGLE lane
       fx_accumulate(acc.l + 0 * kStreamLanes, ratio(g.uy_gt30, g.uy_len));
       fx_accumulate(acc.l + 1 * kStreamLanes, ratio(g.gq_gt30, g.gq_len));
       fx_accumulate(acc.l + 2 * kStreamLanes, ratio(g.gq_sum, g.gq_len));

@@ -35,7 +35,10 @@ struct RecCols {
   const uint8_t* uy_len;
 };
 
-// distinct-count events per record (gene view flags)
+// distinct-count events per record (gene view flags).  The single-read counts are sums of
+// +1 (SINGLE) and -1 (SECOND) events: the sorted pass sets SINGLE on the head of a one-record
+// group; the hash tiles (bucket.h) set SINGLE on every head and SECOND on the record that
+// first finds its group already present.
 enum : uint16_t {
   DF_MOL_HEAD = 1u << 0,
   DF_MOL_SINGLE = 1u << 1,
@@ -43,6 +46,8 @@ enum : uint16_t {
   DF_FRAG_SINGLE = 1u << 3,
   DF_K1_HEAD = 1u << 4,
   DF_K1_MULTI = 1u << 5,
+  DF_MOL_SECOND = 1u << 6,
+  DF_FRAG_SECOND = 1u << 7,
 };
 
 // P_N_MOL, P_MOL_SINGLE, P_N_FRAG, P_FRAG_SINGLE, P_N_K1, P_K1_MULTI, P_MITO_K1

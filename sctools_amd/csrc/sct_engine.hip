@@ -40,7 +40,7 @@ namespace {
 struct Layout {
   size_t tile_cnt, scalars, scan_sums, keys_a, keys_b, vals_a, vals_b, counts, offsets, ent_start, partials;
   size_t gcounts, goffsets, gsums, gwork, dflags, gpay, seen, zero_mito;
-  size_t bdesc, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, total;
+  size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, total;
   int64_t num_tiles, num_chunks, max_ent, max_gene_work, gene_cells, max_seg, max_work;
   int n_buckets;
   bool gene;
@@ -70,8 +70,8 @@ Layout layout_for(const sct_plan_t* plan) {
   L.scan_sums = take(sizeof(uint64_t) * (size_t)(L.num_chunks + 1));
   L.keys_a = take(sizeof(uint64_t) * (size_t)n1);
   L.keys_b = take(sizeof(uint64_t) * (size_t)n1);
-  L.vals_a = take(sizeof(uint32_t) * (size_t)n1);
-  L.vals_b = take(sizeof(uint32_t) * (size_t)n1);
+  L.vals_a = take(sizeof(uint64_t) * (size_t)n1);  // bucket payload w1 (u64); global sort: u32 values
+  L.vals_b = take(sizeof(uint64_t) * (size_t)n1);
   L.counts = take(sizeof(uint32_t) * (size_t)m);
   L.offsets = take(sizeof(uint32_t) * (size_t)m);
   L.ent_start = take(sizeof(int64_t) * (size_t)(L.max_ent + 1));
@@ -88,6 +88,7 @@ Layout layout_for(const sct_plan_t* plan) {
   L.max_seg = n1 / (kBCap + 1) + 2;
   L.max_work = n1 / kChunk + L.max_seg + 2;
   L.bdesc = take(sizeof(uint16_t) * (size_t)n1);
+  L.bent = take(sizeof(uint32_t) * (size_t)n1);
   L.seg_a = take(sizeof(Seg) * (size_t)L.max_seg);
   L.seg_b = take(sizeof(Seg) * (size_t)L.max_seg);
   L.work_a = take(sizeof(Work) * (size_t)L.max_work);
@@ -100,6 +101,10 @@ Layout layout_for(const sct_plan_t* plan) {
 }
 
 size_t count_bytes(const Layout& L) { return L.scalars + 256; }
+
+BucketCtl* bucket_ctl(void* ws, const Layout& L) {
+  return reinterpret_cast<BucketCtl*>(at<uint64_t>(ws, L.scalars) + 8);
+}
 
 int check_plan(const sct_plan_t* plan, const sct_records_t* rec) {
   if (!plan) return fail(SCT_EINVAL, "plan is NULL");
@@ -153,86 +158,98 @@ int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool du
   return SCT_OK;
 }
 
+template <bool kWideK1>
+int launch_hash_tile(bool cell, bool gene, dim3 grid, hipStream_t s, const uint16_t* bdesc, const uint32_t* bent,
+                     const uint64_t* ka, const uint64_t* va, const uint64_t* kb, const uint64_t* vb, int64_t n,
+                     const Bits& b, int64_t* partials, uint16_t* dflags) {
+  if (cell && gene) {
+    LAUNCH("hash_tile", (k_hash_tile<true, true, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb, n,
+           b, partials, dflags);
+  } else if (cell) {
+    LAUNCH("hash_tile", (k_hash_tile<true, false, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb, n,
+           b, partials, dflags);
+  } else {
+    LAUNCH("hash_tile", (k_hash_tile<false, false, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb,
+           n, b, partials, dflags);
+  }
+  return SCT_OK;
+}
+
 // bucket.h driver: level 0 classification, MSD levels until no segment exceeds kBCap, then
-// the tile pass (+ giants).  One host sync per level to size the next level's launches.
-int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const int64_t* ent_start, RecCols r,
+// the hash-tile pass (+ giants).  One host sync per level to size the next level's launches.
+// Returns 1 (not an error code) when build_keys saw a mapped ref id the payload cannot hold:
+// the caller then reruns on the global-sort path.
+int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const int64_t* ent_start,
                     const uint8_t* mito, const Bits& b, bool cell, bool gene, int64_t* partials, uint16_t* dflags,
                     hipStream_t s) {
   if (n == 0) return SCT_OK;
   uint64_t* ka = at<uint64_t>(ws, L.keys_a);
   uint64_t* kb = at<uint64_t>(ws, L.keys_b);
-  uint32_t* va = at<uint32_t>(ws, L.vals_a);
-  uint32_t* vb = at<uint32_t>(ws, L.vals_b);
+  uint64_t* va = at<uint64_t>(ws, L.vals_a);
+  uint64_t* vb = at<uint64_t>(ws, L.vals_b);
   uint16_t* bdesc = at<uint16_t>(ws, L.bdesc);
+  uint32_t* bent = at<uint32_t>(ws, L.bent);
   Seg* seg[2] = {at<Seg>(ws, L.seg_a), at<Seg>(ws, L.seg_b)};
   Work* work[2] = {at<Work>(ws, L.work_a), at<Work>(ws, L.work_b)};
   uint32_t* hist = at<uint32_t>(ws, L.seg_hist);
   uint32_t* cur = at<uint32_t>(ws, L.seg_cur);
   Seg* giants = at<Seg>(ws, L.giants);
-  BucketCtl* ctl = reinterpret_cast<BucketCtl*>(at<uint64_t>(ws, L.scalars) + 8);
+  BucketCtl* ctl = bucket_ctl(ws, L);
   const int KB = b.k1 + b.k2 + b.h;
   HIPCHK(hipMemsetAsync(bdesc, 0, sizeof(uint16_t) * (size_t)n, s));
-  HIPCHK(hipMemsetAsync(ctl, 0, sizeof(BucketCtl), s));
+  HIPCHK(hipMemsetAsync(ctl, 0, 3 * sizeof(uint32_t), s));  // keeps ctl->err from build_keys
   LAUNCH("bucket_level0", k_bucket_level0, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, ent_start, n_ent, n,
-         bdesc, seg[0], work[0], ctl);
+         bdesc, bent, seg[0], work[0], ctl);
   BucketCtl h{};
   HIPCHK(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (h.err) return 1;
   int depth = 0, level = 1, c = 0;
   while (h.n_seg > 0) {
     if ((int64_t)h.n_seg > L.max_seg || (int64_t)h.n_work > L.max_work)
       return fail(SCT_ENOMEM, "bucket level %d: %u segments / %u work items exceed the workspace", level, h.n_seg,
                   h.n_work);
     const int bits = KB - depth < kRadixBits ? KB - depth : kRadixBits;
-    const int shift = KB - depth - bits;
+    const int shift = KB - depth - bits + kKeyShift;
     const int src = (level - 1) & 1;
     const uint64_t* kin = src ? kb : ka;
-    const uint32_t* vin = src ? vb : va;
+    const uint64_t* vin = src ? vb : va;
     uint64_t* kout = src ? ka : kb;
-    uint32_t* vout = src ? va : vb;
+    uint64_t* vout = src ? va : vb;
     HIPCHK(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kRadix * (size_t)h.n_seg, s));
     LAUNCH("bucket_hist", k_bucket_hist, dim3(h.n_work), dim3(kBlock), s, kin, (const Seg*)seg[c],
            (const Work*)work[c], shift, bits, hist);
-    LAUNCH("bucket_segscan", k_bucket_segscan, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c],
-           (const uint32_t*)hist, cur);
-    LAUNCH("bucket_scatter", k_bucket_scatter, dim3(h.n_work), dim3(kBlock), s, kin, vin, kout, vout,
-           (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
     HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), s));  // next level's n_seg, n_work
     LAUNCH("bucket_classify", k_bucket_classify, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c],
-           (const uint32_t*)hist, (const uint32_t*)cur, depth, bits, b.k1, b.k1 + b.k2, KB, level & 1, bdesc,
-           seg[c ^ 1], work[c ^ 1], giants, ctl);
+           (const uint32_t*)hist, cur, depth, bits, b.k1, b.k1 + b.k2, KB, level & 1, bdesc, bent, seg[c ^ 1],
+           work[c ^ 1], giants, ctl);
+    LAUNCH("bucket_scatter", k_bucket_scatter, dim3(h.n_work), dim3(kBlock), s, kin, vin, kout, vout,
+           (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
     HIPCHK(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     c ^= 1;
     depth += bits;
     level++;
   }
-  const int64_t n_win = cdiv(n, kWin);
-  uint32_t* win_ent = at<uint32_t>(ws, L.counts);  // the global-sort count matrix is unused here
-  LAUNCH("bucket_windows", k_window_entities, dim3((unsigned)cdiv(n_win + 1, kBlock)), dim3(kBlock), s, ent_start,
-         n_ent, n, n_win, win_ent);
-  const dim3 tgrid((unsigned)n_win);
-  if (cell && gene) {
-    LAUNCH("bucket_tile", (k_bucket_tile<true, true>), tgrid, dim3(kBlock), s, (const uint16_t*)bdesc, ka, va, kb,
-           vb, n, ent_start, (const uint32_t*)win_ent, r, mito, b, partials, dflags);
-  } else if (cell) {
-    LAUNCH("bucket_tile", (k_bucket_tile<true, false>), tgrid, dim3(kBlock), s, (const uint16_t*)bdesc, ka, va, kb,
-           vb, n, ent_start, (const uint32_t*)win_ent, r, mito, b, partials, dflags);
+  const dim3 tgrid((unsigned)cdiv(n, kWin));
+  int rc;
+  if (b.k1 > kNarrowK1Bits) {
+    rc = launch_hash_tile<true>(cell, gene, tgrid, s, bdesc, bent, ka, va, kb, vb, n, b, partials, dflags);
   } else {
-    LAUNCH("bucket_tile", (k_bucket_tile<false, false>), tgrid, dim3(kBlock), s, (const uint16_t*)bdesc, ka, va,
-           kb, vb, n, ent_start, (const uint32_t*)win_ent, r, mito, b, partials, dflags);
+    rc = launch_hash_tile<false>(cell, gene, tgrid, s, bdesc, bent, ka, va, kb, vb, n, b, partials, dflags);
   }
+  if (rc) return rc;
   if (h.n_giant > 0) {
     const dim3 ggrid(h.n_giant);
     if (cell && gene) {
       LAUNCH("bucket_giant", (k_bucket_giant<true, true>), ggrid, dim3(kBlock), s, (const Seg*)giants, ka, va, kb,
-             vb, r, mito, b, partials, dflags);
+             vb, partials, dflags);
     } else if (cell) {
       LAUNCH("bucket_giant", (k_bucket_giant<true, false>), ggrid, dim3(kBlock), s, (const Seg*)giants, ka, va, kb,
-             vb, r, mito, b, partials, dflags);
+             vb, partials, dflags);
     } else {
       LAUNCH("bucket_giant", (k_bucket_giant<false, false>), ggrid, dim3(kBlock), s, (const Seg*)giants, ka, va, kb,
-             vb, r, mito, b, partials, dflags);
+             vb, partials, dflags);
     }
   }
   return SCT_OK;
@@ -241,9 +258,27 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
 // The RUN-mode pipeline (entity = runs of the cell column, or of the gene column in gene
 // mode; GROUPED runs the cell view).  Writes partial rows into the workspace, output rows
 // if out_i / out_f are set, and grouped gene partials (cell view) if gene_partials is set.
+template <bool kBucket>
+int launch_build_keys(bool cell, bool gene, dim3 grid, hipStream_t s, const KeyCols& kc, const RecCols& rc2,
+                      const uint8_t* mito, int64_t n, const uint64_t* toff, const Bits& b, uint64_t* keys,
+                      void* vals, int64_t* ent_start, int64_t* partials, uint32_t* gcounts, int n_buckets,
+                      uint32_t* err) {
+  if (cell && gene) {
+    LAUNCH("build_keys", (k_build_keys_run<true, true, kBucket>), grid, dim3(kBlock), s, kc, rc2, mito, n, toff, b,
+           keys, vals, ent_start, partials, gcounts, n_buckets, err);
+  } else if (cell) {
+    LAUNCH("build_keys", (k_build_keys_run<true, false, kBucket>), grid, dim3(kBlock), s, kc, rc2, mito, n, toff, b,
+           keys, vals, ent_start, partials, gcounts, n_buckets, err);
+  } else {
+    LAUNCH("build_keys", (k_build_keys_run<false, false, kBucket>), grid, dim3(kBlock), s, kc, rc2, mito, n, toff,
+           b, keys, vals, ent_start, partials, gcounts, n_buckets, err);
+  }
+  return SCT_OK;
+}
+
 int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* gene_is_mito, void* ws,
              size_t ws_bytes, int64_t* out_i, double* out_f, int64_t capacity, int64_t* n_rows,
-             int64_t* gene_partials, hipStream_t s) {
+             int64_t* gene_partials, hipStream_t s, bool allow_bucket = true) {
   const Layout L = layout_for(plan);
   if (!ws || ws_bytes < L.total) return fail(SCT_ENOMEM, "workspace too small (%zu < %zu)", ws_bytes, L.total);
   const int64_t n = rec->n;
@@ -268,7 +303,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   b.k1 = bitlen((uint64_t)(cell ? plan->n_gene_ids : plan->n_cell_ids));
   b.k2 = bitlen((uint64_t)plan->n_umi_ids);
   const char* force = getenv("SCT_FORCE_GLOBAL_SORT");
-  const bool bucket = b.k1 + b.k2 <= kMaxKeyBits && !(force && force[0] == '1');
+  const bool bucket = allow_bucket && b.k1 + b.k2 <= kMaxKeyBits && !(force && force[0] == '1');
   int used;
   if (bucket) {
     b.e = 0;
@@ -312,16 +347,16 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   const int64_t tiles = cdiv(n, kTile);
   const dim3 tgrid((unsigned)tiles);
   const uint64_t* toff = at<uint64_t>(ws, L.tile_cnt);
-  if (cell && gene) {
-    LAUNCH("build_keys", (k_build_keys_run<true, true>), tgrid, dim3(kBlock), s, kc, rc2, mito, n, toff, b, B.ka,
-           B.va, ent_start, partials, gcounts, L.n_buckets);
-  } else if (cell) {
-    LAUNCH("build_keys", (k_build_keys_run<true, false>), tgrid, dim3(kBlock), s, kc, rc2, mito, n, toff, b, B.ka,
-           B.va, ent_start, partials, gcounts, L.n_buckets);
+  if (bucket) {
+    BucketCtl* ctl = bucket_ctl(ws, L);
+    HIPCHK(hipMemsetAsync(ctl, 0, sizeof(BucketCtl), s));
+    rc = launch_build_keys<true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, at<uint64_t>(ws, L.vals_a),
+                                 ent_start, partials, gcounts, L.n_buckets, &ctl->err);
   } else {
-    LAUNCH("build_keys", (k_build_keys_run<false, false>), tgrid, dim3(kBlock), s, kc, rc2, mito, n, toff, b, B.ka,
-           B.va, ent_start, partials, gcounts, L.n_buckets);
+    rc = launch_build_keys<false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va, ent_start, partials,
+                                  gcounts, L.n_buckets, nullptr);
   }
+  if (rc) return rc;
   if (exact && out_i) {  // exact mean / variance lanes of the output rows
     if (cell) {
       LAUNCH("stream_sums", k_stream_sums<true>, tgrid, dim3(kBlock), s, ent_col, rc2, n, toff, partials);
@@ -333,7 +368,10 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   // 2-3. distinct counts (+ per-record distinct events for the gene view)
   uint16_t* dflags = gene ? at<uint16_t>(ws, L.dflags) : nullptr;
   if (bucket) {
-    rc = bucket_distinct(L, ws, n, n_ent, ent_start, rc2, mito, b, cell, gene, partials, dflags, s);
+    rc = bucket_distinct(L, ws, n, n_ent, ent_start, mito, b, cell, gene, partials, dflags, s);
+    if (rc == 1)  // a mapped ref id does not fit the bucket payload: redo on the global-sort path
+      return pipeline(plan, rec, gene_is_mito, ws, ws_bytes, out_i, out_f, capacity, n_rows, gene_partials, s,
+                      false);
     if (rc) return rc;
   } else {
     int which = 0;

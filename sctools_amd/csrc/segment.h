@@ -11,6 +11,7 @@
 // lanes of the quality streams (fixedpt.h).  Runs are contiguous in input order, so
 // a thread flushes once per run it touches and a wave once per tile.
 #pragma once
+#include "bucket.h"
 #include "fixedpt.h"
 #include "radix.h"
 #include "reduce.h"
@@ -120,13 +121,17 @@ __device__ __forceinline__ void tile_run_ids(const int32_t* __restrict__ ent, in
   __syncthreads();
 }
 
-template <bool kCell, bool kGene>
+// kBucket: write the bucket path's 16-byte payload (bucket.h: w0 = key' | ref | strand |
+// mapped, w1 = index | pos; a mapped ref id >= 2^kRefBits raises *err).  Otherwise the
+// global sort's (key with entity bits, u32 value with bit 31 = unmapped).
+template <bool kCell, bool kGene, bool kBucket>
 __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r, const uint8_t* __restrict__ k1_is_mito,
                                                            int64_t n, const uint64_t* __restrict__ tile_off, Bits b,
-                                                           uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                           uint64_t* __restrict__ keys, void* __restrict__ vals,
                                                            int64_t* __restrict__ ent_start,
                                                            int64_t* __restrict__ partials,
-                                                           uint32_t* __restrict__ gene_counts, int n_buckets) {
+                                                           uint32_t* __restrict__ gene_counts, int n_buckets,
+                                                           uint32_t* __restrict__ err) {
   static_assert(!kGene || kCell, "gene buckets come from the cell view");
   __shared__ int32_t s_e[kTile];
   __shared__ int32_t s_prev;
@@ -160,9 +165,19 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
     const uint8_t bt = r.bits[p];
     const uint8_t xf = r.xf[p];
     const bool mapped = !(bt & SCT_B_UNMAPPED);
-    const uint32_t hsh = mapped ? frag_hash(r.ref[p], r.pos[p], (bt & SCT_B_REVERSE) ? 1u : 0u) : 0u;
-    keys[p] = make_key((uint64_t)e, k1, k2, hsh, b);
-    vals[p] = (uint32_t)p | (mapped ? 0u : kUnmappedValBit);
+    const int32_t ref = r.ref[p];
+    const int32_t pos = r.pos[p];
+    const bool rev = bt & SCT_B_REVERSE;
+    const uint32_t hsh = mapped ? frag_hash(ref, pos, rev ? 1u : 0u) : 0u;
+    if constexpr (kBucket) {
+      const bool mito = kCell ? k1_is_mito[k1] != 0 : false;
+      keys[p] = payload_w0(make_key(0, k1, k2, hsh, b), ref, rev, mapped, mito);
+      static_cast<uint64_t*>(vals)[p] = ((uint64_t)p << 32) | (uint32_t)pos;
+      if (mapped && (uint32_t)ref >= (1u << kRefBits)) atomicOr(err, 1u);
+    } else {
+      keys[p] = make_key((uint64_t)e, k1, k2, hsh, b);
+      static_cast<uint32_t*>(vals)[p] = (uint32_t)p | (mapped ? 0u : kUnmappedValBit);
+    }
     // MetricAggregator.parse_molecule (aggregator.py:259-334)
     acc.v[0] += 1;
     acc.v[1] += (bt & SCT_B_PERFECT_UMI) ? 1 : 0;

@@ -142,6 +142,58 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* total, T* lds) {
   return res;
 }
 
+// block_exclusive_scan for a block of NT threads; `lds` needs NT / 64 + 1 entries.
+template <int NT, typename T>
+__device__ __forceinline__ T block_exclusive_scan_n(T v, T* total, T* lds) {
+  constexpr int W = NT / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  T x = v;
+  for (int off = 1; off < kWave; off <<= 1) {
+    T y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == kWave - 1) lds[wid] = x;
+  __syncthreads();
+  if (threadIdx.x < kWave) {  // wave 0 scans the W wave totals
+    T w = threadIdx.x < W ? lds[threadIdx.x] : (T)0;
+    T s = w;
+    for (int off = 1; off < W; off <<= 1) {
+      T y = __shfl_up(s, off);
+      if ((int)threadIdx.x >= off) s += y;
+    }
+    if (threadIdx.x < W) lds[threadIdx.x] = s - w;
+    if (threadIdx.x == W - 1) lds[W] = s;
+  }
+  __syncthreads();
+  T res = lds[wid] + x - v;
+  *total = lds[W];
+  __syncthreads();
+  return res;
+}
+
+// exclusive max-scan (values >= 0) for a block of NT threads; `lds` needs NT / 64 entries
+template <int NT>
+__device__ __forceinline__ uint32_t block_exclusive_max_n(uint32_t v, uint32_t* lds) {
+  constexpr int W = NT / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  uint32_t x = v;
+  for (int off = 1; off < kWave; off <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, off);
+    if (lane >= off) x = y > x ? y : x;
+  }
+  if (lane == kWave - 1) lds[wid] = x;
+  __syncthreads();
+  uint32_t carry = 0;
+  for (int w = 0; w < wid; w++) carry = lds[w] > carry ? lds[w] : carry;
+  uint32_t ex = (uint32_t)__shfl_up((int)x, 1);
+  if (lane == 0) ex = 0;
+  __syncthreads();
+  (void)W;
+  return ex > carry ? ex : carry;
+}
+
 // a / b of two small non-negative integers, correctly rounded (Python int / int);
 // 0 for b == 0 (only reached by records the reference never aggregates)
 __device__ __forceinline__ double ratio(uint32_t a, uint32_t b) { return b ? (double)a / (double)b : 0.0; }
@@ -168,8 +220,49 @@ namespace sct {
 // 0..K-1 add slot SlotOf(i) of that entity's row with ONE atomic instruction (K
 // contiguous-ish int64 adds) instead of K single-lane instructions per lane.
 // Members' v[] are cleared.  Every lane of the wave must call it.
-template <int K, typename SlotOf>
-__device__ __forceinline__ void wave_flush(int64_t (&v)[K], bool member, int64_t e, int64_t* __restrict__ rows,
+// DPP wave reduction (GFX9 quad_perm / row_shr / row_bcast): the sum of all 64 lanes, returned
+// uniformly.  Every lane must be active.  No LDS traffic, unlike __shfl_xor (ds_bpermute).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int32_t dpp_i32(int32_t v) {
+  return __builtin_amdgcn_update_dpp(0, v, kCtrl, kRowMask, 0xf, false);
+}
+__device__ __forceinline__ int32_t wave_sum_dpp(int32_t v) {
+  v += dpp_i32<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dpp_i32<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dpp_i32<0x114, 0xf>(v);  // row_shr:4
+  v += dpp_i32<0x118, 0xf>(v);  // row_shr:8  -> lane 15 of each row holds the row sum
+  v += dpp_i32<0x142, 0xa>(v);  // row_bcast:15 -> lanes 31 / 63 hold two-row sums
+  v += dpp_i32<0x143, 0xc>(v);  // row_bcast:31 -> lane 63 holds the wave sum
+  return __builtin_amdgcn_readlane(v, 63);
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ int64_t dpp_i64(int64_t v) {
+  const uint32_t lo = (uint32_t)dpp_i32<kCtrl, kRowMask>((int32_t)(uint32_t)v);
+  const uint32_t hi = (uint32_t)dpp_i32<kCtrl, kRowMask>((int32_t)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t wave_sum_dpp(int64_t v) {
+  v += dpp_i64<0xb1, 0xf>(v);
+  v += dpp_i64<0x4e, 0xf>(v);
+  v += dpp_i64<0x114, 0xf>(v);
+  v += dpp_i64<0x118, 0xf>(v);
+  v += dpp_i64<0x142, 0xa>(v);
+  v += dpp_i64<0x143, 0xc>(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)v, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)((uint64_t)v >> 32), 63);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Wave-cooperative flush of per-lane partial sums into int64 rows.
+//
+// Lanes with `member` set hold partial sums v[0..K) for entity `e` (per lane).  For every
+// distinct entity among the members (a wave-uniform loop; one iteration when the wave
+// is inside one entity), the members' values are summed across the wave (DPP) and lanes
+// 0..K-1 add slot SlotOf(i) of that entity's row with ONE atomic instruction instead of K
+// single-lane instructions per lane.  Members' v[] are cleared.  Every lane of the wave must
+// call it with all lanes active.  T = int32_t or int64_t.
+template <int K, typename T, typename SlotOf>
+__device__ __forceinline__ void wave_flush(T (&v)[K], bool member, int64_t e, int64_t* __restrict__ rows,
                                            SlotOf slot_of) {
   static_assert(K <= kWave, "one lane per slot");
   const int lane = threadIdx.x & (kWave - 1);
@@ -181,8 +274,8 @@ __device__ __forceinline__ void wave_flush(int64_t (&v)[K], bool member, int64_t
     int64_t mine = 0;
 #pragma unroll
     for (int i = 0; i < K; i++) {
-      const int64_t tot = wave_sum(in ? v[i] : (int64_t)0);
-      mine = (lane == i) ? tot : mine;
+      const T tot = wave_sum_dpp(in ? v[i] : (T)0);
+      mine = (lane == i) ? (int64_t)tot : mine;
     }
     if (lane < K && mine) atomicAdd((unsigned long long*)&rows[el * SCT_NP + slot_of(lane)], (unsigned long long)mine);
     if (in) {

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--cells", type=int, default=10_000)
     ap.add_argument("--genes", type=int, default=30_000)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--only", default="", help="comma-separated variant names")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     eng = E.get_engine(dev)
@@ -34,6 +35,8 @@ def main():
         "cell_welford": lambda: eng.compute(d.cols, "cell", dims, mito, mito, float_mode="welford", n_entities=n_ent),
         "cell_and_gene": lambda: eng.cell_and_gene(d.cols, dims, mito, n_entities=n_ent),
     }
+    if a.only:
+        variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
     out = {}
     for name, fn in variants.items():
         fn()

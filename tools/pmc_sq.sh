@@ -2,7 +2,9 @@
 set -e
 R=$GRAFT_REPO_ROOT
 export TMPDIR=/tmp
+O=$R/gpurun_out/${1:-pmc_sq}
+mkdir -p $O
 cd /tmp
-rocprofv3 -L > $R/gpurun_out/counters_list.txt 2>&1 || true
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $R/gpurun_out/pmc_sq -o sq1 -- python3 $R/tools/pmc_probe.py --reps 1 > $R/gpurun_out/pmc_sq1.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES --output-format csv -d $R/gpurun_out/pmc_sq -o sq2 -- python3 $R/tools/pmc_probe.py --reps 1 > $R/gpurun_out/pmc_sq2.log 2>&1
+timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $O -o sq1 -- python3 $R/tools/pmc_probe.py --reps 1 > $O/sq1.log 2>&1
+timeout -k 10 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv -d $O -o sq2 -- python3 $R/tools/pmc_probe.py --reps 1 > $O/sq2.log 2>&1
+find $O -name "*counter_collection.csv" | head
