@@ -85,8 +85,7 @@ struct __attribute__((aligned(16))) GenePayload {
 };
 static_assert(sizeof(GenePayload) == 16, "gene payload must be 16 bytes");
 
-constexpr int kGenesPerBucket = 128;  // LDS bins of one gene bucket
-constexpr int kMaxGeneBuckets = 2048;
-constexpr int kGeneLanes = 1 + kGeneFlags + 3 * 8;  // n_reads, 14 flag counts, 3 streams x 8 lanes
+constexpr int kGenesPerBucket = 64;  // LDS bins of one gene bucket
+constexpr int kMaxGeneBuckets = 2048;  // n_gene_ids <= 131072
 
 }  // namespace sct

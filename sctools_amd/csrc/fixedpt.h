@@ -62,9 +62,9 @@ SCT_HD uint64_t dbits(double x) {
 SCT_HD void fx_accumulate(int64_t* lanes, double x) {
   const uint64_t b = dbits(x);
   const int ex = (int)((b >> 52) & 0x7ff);
-  if (ex == 0) return;  // x == 0
-  const uint64_t m = (b & 0xFFFFFFFFFFFFFull) | (1ull << 52);
-  const int s = ex - 1007;  // X = m << s, 0 <= s <= 31
+  // x == 0 adds zeros (branch-free: m = 0, s = 0)
+  const uint64_t m = ex ? ((b & 0xFFFFFFFFFFFFFull) | (1ull << 52)) : 0ull;
+  const int s = ex ? ex - 1007 : 0;  // X = m << s, 0 <= s <= 31
   const uint64_t lo = m << s;
   const uint64_t hi = s ? (m >> (64 - s)) : 0;
   lanes[0] += (int64_t)(lo & 0xffffffffu);
