@@ -78,6 +78,9 @@ struct Welford {
 template <bool kCell>
 __global__ void k_welford(RecCols r, const int64_t* __restrict__ ent_start, int64_t n_ent, int64_t n,
                           double* __restrict__ out_f) {
+  __shared__ double s_rcp[kRcpN];
+  fill_rcp(s_rcp);
+  __syncthreads();
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n_ent) return;
   const int64_t s = ent_start[e];
@@ -87,10 +90,10 @@ __global__ void k_welford(RecCols r, const int64_t* __restrict__ ent_start, int6
   for (int64_t i = s; i < t; i++) {
     cnt += 1.0;
     const uint32_t gl = r.gq_len[i];
-    if (kCell) wc.update(ratio(r.cy_gt30[i], r.cy_len[i]), cnt);
-    wu.update(ratio(r.uy_gt30[i], r.uy_len[i]), cnt);
-    wf.update(ratio(r.gq_gt30[i], gl), cnt);
-    wq.update(ratio(r.gq_sum[i], gl), cnt);
+    if (kCell) wc.update(ratio_rcp(r.cy_gt30[i], r.cy_len[i], s_rcp), cnt);
+    wu.update(ratio_rcp(r.uy_gt30[i], r.uy_len[i], s_rcp), cnt);
+    wf.update(ratio_rcp(r.gq_gt30[i], gl, s_rcp), cnt);
+    wq.update(ratio_rcp(r.gq_sum[i], gl, s_rcp), cnt);
   }
   const double qnan = __builtin_nan("");
   const double dn1 = cnt - 1.0;

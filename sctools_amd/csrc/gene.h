@@ -4,10 +4,10 @@
 // plain per-record sums plus distinct counts over (gene, cell, umi) keys.  Those keys
 // are the cell view's (cell, gene, umi) keys, so the distinct-count events come from
 // the cell-view sorted pass (reduce.h, DF_* flags by record index).  Here:
+//   k_gene_plan    bucket starts from the per-bucket record counts (build_keys) -> the
+//                  emit cursors and the reduce work list;
 //   k_gene_emit    input order, coalesced: one 16-byte GenePayload per record into its
-//                  gene bucket (kGenesPerBucket genes) at offsets from the per-tile
-//                  bucket count matrix (segment.h) -- no atomics across blocks;
-//   k_gene_plan    bucket extents -> block work list;
+//                  gene bucket (kGenesPerBucket genes), one cursor atomic per (block, bucket);
 //   k_gene_reduce  each block counting-sorts sub-tiles of one bucket's payloads by gene in
 //                  LDS, sums each thread's runs of equal gene in registers, adds runs into
 //                  LDS bins, and the bins into the rows.
@@ -22,7 +22,10 @@
 namespace sct {
 
 constexpr int kGeneChunk = 16384;  // payloads per reduce block
-constexpr int kGeneSub = 1024;     // payloads sorted in LDS at a time
+#ifndef SCT_GENE_SUB
+#define SCT_GENE_SUB 2048
+#endif
+constexpr int kGeneSub = SCT_GENE_SUB;  // payloads sorted in LDS at a time
 constexpr int kGeneItems = kGeneSub / kBlock;
 constexpr int kGeneCnt = 1 + kGeneFlags;  // n_reads + flag counts (32-bit bins)
 constexpr int kGeneCntPad = 16;
@@ -50,83 +53,122 @@ __device__ __forceinline__ uint32_t block_rank(uint32_t key, int nbits, bool val
   return base + (uint32_t)__popcll(peers & lt);
 }
 
+// one 16-byte payload per record: everything GatherGeneMetrics derives from the record
+__device__ __forceinline__ uint4 gene_payload(uint32_t g, uint8_t bt, uint8_t xf, uint16_t df, uint8_t uy_gt30,
+                                              uint8_t uy_len, uint16_t gq_gt30, uint16_t gq_len, uint16_t gq_sum) {
+  uint32_t f = (bt & SCT_B_PERFECT_UMI) ? GF_PERFECT_UMI : 0;
+  if (!(bt & SCT_B_UNMAPPED)) {
+    f |= (xf == SCT_XF_CODING ? GF_EXONIC : 0) | (xf == SCT_XF_INTRONIC ? GF_INTRONIC : 0) |
+         (xf == SCT_XF_UTR ? GF_UTR : 0) | ((bt & SCT_B_NH1) ? GF_UNIQUE : GF_MULTIPLE) |
+         ((bt & SCT_B_DUPLICATE) ? GF_DUP : 0) | ((bt & SCT_B_SPLICED) ? GF_SPLICED : 0);
+  }
+  f |= (df & DF_MOL_HEAD ? GF_MOL_HEAD : 0) | (df & DF_MOL_SINGLE ? GF_MOL_SINGLE : 0) |
+       (df & DF_FRAG_FIRST ? GF_FRAG_FIRST : 0) | (df & DF_FRAG_SINGLE ? GF_FRAG_SINGLE : 0) |
+       (df & DF_K1_HEAD ? GF_CG_HEAD : 0) | (df & DF_K1_MULTI ? GF_CG_MULTI : 0) |
+       (df & DF_MOL_SECOND ? GF_MOL_SECOND : 0) | (df & DF_FRAG_SECOND ? GF_FRAG_SECOND : 0);
+  GenePayload gp;
+  gp.gene = g;
+  gp.flags = (uint16_t)f;
+  gp.uy_gt30 = uy_gt30;
+  gp.uy_len = uy_len;
+  gp.gq_gt30 = gq_gt30;
+  gp.gq_len = gq_len;
+  gp.gq_sum = gq_sum;
+  gp.pad = 0;
+  return *reinterpret_cast<const uint4*>(&gp);
+}
+
+// One block per kEmitTile records (input order, coalesced).  (1) rank every record among the
+// block's records of its gene bucket (wave-aggregated LDS counters); (2) reserve one range per
+// present bucket with one atomic on the bucket's cursor (k_gene_plan set it to the bucket's
+// start); (3) re-read the columns, build the payloads and write each at its range + rank.
+// The order inside a bucket region is therefore arbitrary; the reduction is order-free.
+constexpr int kEmitTile = 4 * kTile;
+constexpr int kEmitItems = kEmitTile / kBlock;
+static_assert(kEmitTile <= 65536, "ranks are 16-bit");
 __global__ void __launch_bounds__(kBlock) k_gene_emit(const int32_t* __restrict__ gene, RecCols r,
                                                       const uint16_t* __restrict__ dflags, int64_t n,
-                                                      const uint32_t* __restrict__ offsets, int n_buckets,
+                                                      uint32_t* __restrict__ cursor, int n_buckets,
                                                       GenePayload* __restrict__ pay) {
   __shared__ uint32_t s_cnt[kMaxGeneBuckets];
   __shared__ uint32_t s_off[kMaxGeneBuckets];
+  __shared__ uint16_t s_rank[kEmitTile];
   const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kTile;
-  const int64_t tiles = gridDim.x;
+  const int64_t base = (int64_t)blockIdx.x * kEmitTile;
   int nbb = 0;
   while ((1 << nbb) < n_buckets) nbb++;
+  for (int i = t; i < n_buckets; i += kBlock) s_cnt[i] = 0;
+  __syncthreads();
+#pragma unroll 4
+  for (int j = 0; j < kEmitItems; j++) {
+    const int q = j * kBlock + t;
+    const int64_t p = base + q;
+    const bool valid = p < n;
+    const uint32_t bk = valid ? (uint32_t)gene[p] / kGenesPerBucket : 0u;
+    const uint32_t rank = block_rank(bk, nbb, valid, s_cnt);
+    s_rank[q] = (uint16_t)rank;
+  }
+  __syncthreads();
   for (int i = t; i < n_buckets; i += kBlock) {
-    s_cnt[i] = 0;
-    s_off[i] = offsets[(int64_t)i * tiles + blockIdx.x];
+    const uint32_t c = s_cnt[i];
+    if (c) s_off[i] = atomicAdd(&cursor[i], c);
   }
   __syncthreads();
 #pragma unroll 4
-  for (int j = 0; j < kItems; j++) {
-    const int64_t p = base + (int64_t)j * kBlock + t;
-    const bool valid = p < n;
-    GenePayload gp{};
-    uint32_t bk = 0;
-    if (valid) {
-      const uint32_t g = (uint32_t)gene[p];
-      const uint8_t bt = r.bits[p];
-      const uint8_t xf = r.xf[p];
-      const uint16_t df = dflags[p];
-      uint32_t f = (bt & SCT_B_PERFECT_UMI) ? GF_PERFECT_UMI : 0;
-      if (!(bt & SCT_B_UNMAPPED)) {
-        f |= (xf == SCT_XF_CODING ? GF_EXONIC : 0) | (xf == SCT_XF_INTRONIC ? GF_INTRONIC : 0) |
-             (xf == SCT_XF_UTR ? GF_UTR : 0) | ((bt & SCT_B_NH1) ? GF_UNIQUE : GF_MULTIPLE) |
-             ((bt & SCT_B_DUPLICATE) ? GF_DUP : 0) | ((bt & SCT_B_SPLICED) ? GF_SPLICED : 0);
-      }
-      f |= (df & DF_MOL_HEAD ? GF_MOL_HEAD : 0) | (df & DF_MOL_SINGLE ? GF_MOL_SINGLE : 0) |
-           (df & DF_FRAG_FIRST ? GF_FRAG_FIRST : 0) | (df & DF_FRAG_SINGLE ? GF_FRAG_SINGLE : 0) |
-           (df & DF_K1_HEAD ? GF_CG_HEAD : 0) | (df & DF_K1_MULTI ? GF_CG_MULTI : 0) |
-           (df & DF_MOL_SECOND ? GF_MOL_SECOND : 0) | (df & DF_FRAG_SECOND ? GF_FRAG_SECOND : 0);
-      gp.gene = g;
-      gp.flags = (uint16_t)f;
-      gp.uy_gt30 = r.uy_gt30[p];
-      gp.uy_len = r.uy_len[p];
-      gp.gq_gt30 = r.gq_gt30[p];
-      gp.gq_len = r.gq_len[p];
-      gp.gq_sum = r.gq_sum[p];
-      gp.pad = 0;
-      bk = g / kGenesPerBucket;
-    }
-    const uint32_t rank = block_rank(bk, nbb, valid, s_cnt);
-    if (valid) reinterpret_cast<uint4*>(pay)[(uint64_t)s_off[bk] + rank] = *reinterpret_cast<const uint4*>(&gp);
+  for (int j = 0; j < kEmitItems; j++) {
+    const int q = j * kBlock + t;
+    const int64_t p = base + q;
+    if (p >= n) break;
+    const uint32_t g = (uint32_t)gene[p];
+    const uint4 w = gene_payload(g, r.bits[p], r.xf[p], dflags[p], r.uy_gt30[p], r.uy_len[p], r.gq_gt30[p],
+                                 r.gq_len[p], r.gq_sum[p]);
+    reinterpret_cast<uint4*>(pay)[(uint64_t)s_off[g / kGenesPerBucket] + s_rank[q]] = w;
   }
 }
 
-// one block: bucket extents from the scanned count matrix -> block work list
-__global__ void k_gene_plan(const uint32_t* __restrict__ offsets, int64_t tiles, int n_buckets, int64_t n,
-                            int64_t* __restrict__ work, int64_t* __restrict__ n_work) {
+// one block: bucket starts (exclusive scan of the bucket counts) -> the emit cursors and the
+// reduce work list (chunks of <= kGeneChunk payloads of one bucket), written by all threads
+__global__ void __launch_bounds__(kBlock) k_gene_plan(const uint32_t* __restrict__ counts, int n_buckets,
+                                                      uint32_t* __restrict__ cursor, int64_t* __restrict__ work,
+                                                      int64_t* __restrict__ n_work) {
   __shared__ uint64_t lds[kWaves + 1];
-  uint64_t carry_w = 0;
+  __shared__ uint32_t s_beg[kMaxGeneBuckets + 1];
+  __shared__ uint32_t s_woff[kMaxGeneBuckets + 1];
+  uint64_t carry = 0, carry_w = 0;
   for (int base = 0; base < n_buckets; base += kBlock) {
     const int bk = base + threadIdx.x;
-    uint64_t beg = 0, end = 0;
-    if (bk < n_buckets) {
-      beg = offsets[(int64_t)bk * tiles];
-      end = bk + 1 < n_buckets ? offsets[(int64_t)(bk + 1) * tiles] : (uint64_t)n;
-    }
-    const uint64_t nw = (end - beg + kGeneChunk - 1) / kGeneChunk;
+    const uint64_t c = bk < n_buckets ? counts[bk] : 0;
+    uint64_t tot;
+    const uint64_t beg = block_exclusive_scan<uint64_t>(c, &tot, lds) + carry;
+    carry += tot;
+    const uint64_t nw = (c + kGeneChunk - 1) / kGeneChunk;
     uint64_t tot_w;
     const uint64_t woff = block_exclusive_scan<uint64_t>(nw, &tot_w, lds) + carry_w;
-    for (uint64_t k = 0; k < nw; k++) {
-      const uint64_t b0 = beg + k * kGeneChunk;
-      const uint64_t b1 = (b0 + kGeneChunk < end) ? b0 + kGeneChunk : end;
-      work[3 * (woff + k) + 0] = bk;
-      work[3 * (woff + k) + 1] = (int64_t)b0;
-      work[3 * (woff + k) + 2] = (int64_t)b1;
-    }
     carry_w += tot_w;
+    if (bk < n_buckets) {
+      cursor[bk] = (uint32_t)beg;
+      s_beg[bk] = (uint32_t)beg;
+      s_woff[bk] = (uint32_t)woff;
+    }
   }
-  if (threadIdx.x == 0) *n_work = (int64_t)carry_w;
+  if (threadIdx.x == 0) {
+    s_beg[n_buckets] = (uint32_t)carry;
+    s_woff[n_buckets] = (uint32_t)carry_w;
+    *n_work = (int64_t)carry_w;
+  }
+  __syncthreads();
+  for (uint32_t w = threadIdx.x; w < (uint32_t)carry_w; w += kBlock) {
+    int lo = 0, hi = n_buckets - 1;  // the bucket with s_woff[b] <= w < s_woff[b + 1]
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) / 2;
+      if (s_woff[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const uint64_t b0 = (uint64_t)s_beg[lo] + (uint64_t)(w - s_woff[lo]) * kGeneChunk;
+    const uint64_t e = s_beg[lo + 1];
+    work[3 * w + 0] = lo;
+    work[3 * w + 1] = (int64_t)b0;
+    work[3 * w + 2] = (int64_t)(b0 + kGeneChunk < e ? b0 + kGeneChunk : e);
+  }
 }
 
 struct GeneAcc {
@@ -138,15 +180,15 @@ struct GeneAcc {
 #pragma unroll
     for (int i = 0; i < 3 * kStreamLanes; i++) l[i] = 0;
   }
-  __device__ __forceinline__ void add(const GenePayload& g, double x0, double x1, double x2) {
+  __device__ __forceinline__ void add(const GenePayload& g, const double* s_rcp) {
     c[0] += 1;
 #pragma unroll
     for (int f = 0; f < kGeneFlags; f++) c[1 + f] += (g.flags >> f) & 1u;
     c[1 + 9] -= (g.flags >> 14) & 1u;   // GF_MOL_SECOND on the GF_MOL_SINGLE lane
     c[1 + 11] -= (g.flags >> 15) & 1u;  // GF_FRAG_SECOND on the GF_FRAG_SINGLE lane
-    fx_accumulate(l + 0 * kStreamLanes, x0);
-    fx_accumulate(l + 1 * kStreamLanes, x1);
-    fx_accumulate(l + 2 * kStreamLanes, x2);
+    fx_accumulate(l + 0 * kStreamLanes, ratio_rcp(g.uy_gt30, g.uy_len, s_rcp));
+    fx_accumulate(l + 1 * kStreamLanes, ratio_rcp(g.gq_gt30, g.gq_len, s_rcp));
+    fx_accumulate(l + 2 * kStreamLanes, ratio_rcp(g.gq_sum, g.gq_len, s_rcp));
   }
   __device__ __forceinline__ void flush(int32_t* cbin, unsigned long long* lbin) const {
 #pragma unroll
@@ -160,7 +202,10 @@ struct GeneAcc {
 
 // One work item = (gene bucket, range of its payloads).  Each sub-tile of kGeneSub payloads is
 // counting-sorted in LDS by local gene id, so every thread's kGeneItems consecutive payloads are
-// long runs of one gene: registers accumulate a run and flush it into the LDS bins once.
+// long runs of one gene: registers accumulate a run and flush it into the LDS bins once.  The
+// run survives sub-tiles: sorted sub-tiles of one bucket put the same genes at similar
+// positions, so a thread keeps adding to one gene and flushes on change.  (The flushes -- 39
+// LDS atomics per finished run -- are most of the kernel's time; see DESIGN.md.)
 __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __restrict__ pay,
                                                         const int64_t* __restrict__ work,
                                                         const int64_t* __restrict__ n_work, int32_t n_gene_ids,
@@ -171,8 +216,10 @@ __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __res
   __shared__ uint32_t s_cnt[kGenesPerBucket];
   __shared__ uint32_t s_start[kGenesPerBucket];
   __shared__ uint64_t s_scan[kWaves + 1];
+  __shared__ double s_rcp[kRcpN];
   if ((int64_t)blockIdx.x >= *n_work) return;  // block-uniform
   const int t = threadIdx.x;
+  fill_rcp(s_rcp);  // visible after the first sub-tile's barriers
   const int bucket = (int)work[3 * blockIdx.x + 0];
   const int64_t beg = work[3 * blockIdx.x + 1];
   const int64_t end = work[3 * blockIdx.x + 2];
@@ -180,28 +227,27 @@ __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __res
   for (int i = t; i < kGenesPerBucket * kGeneCntPad; i += kBlock) s_cbin[i] = 0;
   for (int i = t; i < kGenesPerBucket * 3 * kStreamLanes; i += kBlock) s_lbin[i] = 0ull;
   const uint4* src = reinterpret_cast<const uint4*>(pay);
-  // A thread's run accumulator survives sub-tiles: sorted sub-tiles of one bucket put the same
-  // genes at similar positions, so a thread keeps adding to one gene and flushes on change.
   GeneAcc acc;
   acc.clear();
   int cur = -1;
   for (int64_t sub = beg; sub < end; sub += kGeneSub) {
     const int cnt = (int)((end - sub) < kGeneSub ? (end - sub) : kGeneSub);
     if (t < kGenesPerBucket) s_cnt[t] = 0;
-    uint4 v[kGeneItems];
-    uint32_t rk[kGeneItems];
+    // rank on the gene word alone (clamped, unconditional loads: all in flight at once), then
+    // re-read the whole payload for the LDS scatter (an L2 hit) -- 2 live VGPRs per item
+    const uint32_t* gw = reinterpret_cast<const uint32_t*>(src + sub);
+    uint32_t vx[kGeneItems], rk[kGeneItems];
 #pragma unroll
     for (int j = 0; j < kGeneItems; j++) {
       const int q = j * kBlock + t;
-      if (q < cnt) v[j] = src[sub + q];
+      vx[j] = gw[4 * (q < cnt ? q : cnt - 1)];  // GenePayload.gene is the first word
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kGeneItems; j++) {
       const int q = j * kBlock + t;
       const bool valid = q < cnt;
-      const uint32_t lg = valid ? v[j].x - g0 : 0u;  // GenePayload.gene is the first word
-      rk[j] = block_rank(lg, 6, valid, s_cnt);
+      rk[j] = block_rank(valid ? vx[j] - g0 : 0u, 6, valid, s_cnt);
     }
     __syncthreads();
     {
@@ -214,41 +260,22 @@ __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __res
 #pragma unroll
     for (int j = 0; j < kGeneItems; j++) {
       const int q = j * kBlock + t;
-      if (q < cnt) s_sorted[s_start[v[j].x - g0] + rk[j]] = v[j];
+      if (q < cnt) s_sorted[s_start[vx[j] - g0] + rk[j]] = src[sub + q];
     }
     __syncthreads();
-    // the thread's kGeneItems sorted payloads; all divisions first (independent, overlapped)
+    // the thread's kGeneItems consecutive sorted payloads
     const int j0 = t * kGeneItems;
-    GenePayload gs[kGeneItems];
-    double xs[kGeneItems][3];
-#pragma unroll
-    for (int k = 0; k < kGeneItems; k++) {
-      const uint4 w = j0 + k < cnt ? s_sorted[j0 + k] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
-      gs[k] = *reinterpret_cast<const GenePayload*>(&w);
-#ifndef SCT_EXP_NO_DIV
-      xs[k][0] = ratio(gs[k].uy_gt30, gs[k].uy_len);
-      xs[k][1] = ratio(gs[k].gq_gt30, gs[k].gq_len);
-      xs[k][2] = ratio(gs[k].gq_sum, gs[k].gq_len);
-#else
-      xs[k][0] = (double)gs[k].uy_gt30;
-      xs[k][1] = (double)gs[k].gq_gt30;
-      xs[k][2] = (double)gs[k].gq_sum;
-#endif
-    }
-#pragma unroll
-    for (int k = 0; k < kGeneItems; k++) {
-      if (j0 + k >= cnt) break;
-      const int lg = (int)(gs[k].gene - g0);
+    const int my_n = cnt - j0 < 0 ? 0 : (cnt - j0 < kGeneItems ? cnt - j0 : kGeneItems);
+    for (int k = 0; k < my_n; k++) {
+      const uint4 w = s_sorted[j0 + k];
+      const GenePayload& g = *reinterpret_cast<const GenePayload*>(&w);
+      const int lg = (int)(g.gene - g0);
       if (lg != cur) {
         if (cur >= 0) acc.flush(&s_cbin[cur * kGeneCntPad], &s_lbin[cur * 3 * kStreamLanes]);
         acc.clear();
         cur = lg;
       }
-#ifndef SCT_EXP_SORT_ONLY
-      acc.add(gs[k], xs[k][0], xs[k][1], xs[k][2]);
-#else
-      acc.c[0] += (int)xs[k][0];
-#endif
+      acc.add(g, s_rcp);
     }
     __syncthreads();  // s_sorted / s_cnt are reused by the next sub-tile
   }

@@ -39,9 +39,9 @@ namespace {
 
 struct Layout {
   size_t tile_cnt, scalars, scan_sums, keys_a, keys_b, vals_a, vals_b, counts, offsets, ent_start, partials;
-  size_t gcounts, goffsets, gsums, gwork, dflags, gpay, seen, zero_mito;
+  size_t gcounts, gcursor, gwork, dflags, gpay, seen, zero_mito;
   size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, total;
-  int64_t num_tiles, num_chunks, max_ent, max_gene_work, gene_cells, max_seg, max_work;
+  int64_t num_tiles, num_chunks, max_ent, max_gene_work, max_seg, max_work;
   int n_buckets;
   bool gene;
 };
@@ -57,7 +57,6 @@ Layout layout_for(const sct_plan_t* plan) {
   L.gene = plan->mode == SCT_MODE_GENE_GROUPED || (plan->flags & SCT_PLAN_GENE_PARTIALS);
   L.n_buckets = (int)cdiv(plan->n_gene_ids > 0 ? plan->n_gene_ids : 1, kGenesPerBucket);
   L.max_gene_work = L.n_buckets + cdiv(n1, kGeneChunk) + 1;
-  L.gene_cells = (int64_t)L.n_buckets * L.num_tiles;  // per-tile gene-bucket count matrix
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -76,9 +75,8 @@ Layout layout_for(const sct_plan_t* plan) {
   L.offsets = take(sizeof(uint32_t) * (size_t)m);
   L.ent_start = take(sizeof(int64_t) * (size_t)(L.max_ent + 1));
   L.partials = take(sizeof(int64_t) * SCT_NP * (size_t)L.max_ent);
-  L.gcounts = take(L.gene ? sizeof(uint32_t) * (size_t)L.gene_cells : 0);
-  L.goffsets = take(L.gene ? sizeof(uint32_t) * (size_t)L.gene_cells : 0);
-  L.gsums = take(L.gene ? sizeof(uint64_t) * (size_t)(cdiv(L.gene_cells, kScanChunk) + 1) : 0);
+  L.gcounts = take(L.gene ? sizeof(uint32_t) * (size_t)L.n_buckets : 0);  // records per gene bucket
+  L.gcursor = take(L.gene ? sizeof(uint32_t) * (size_t)L.n_buckets : 0);
   L.gwork = take(L.gene ? sizeof(int64_t) * 3 * (size_t)L.max_gene_work : 0);
   L.dflags = take(L.gene ? sizeof(uint16_t) * (size_t)n1 : 0);
   L.gpay = take(L.gene ? sizeof(GenePayload) * (size_t)n1 : 0);
@@ -342,6 +340,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     mito = z;
   }
   HIPCHK(hipMemsetAsync(partials, 0, sizeof(int64_t) * SCT_NP * (size_t)n_ent, s));
+  if (gene) HIPCHK(hipMemsetAsync(gcounts, 0, sizeof(uint32_t) * (size_t)L.n_buckets, s));
 
   // 1. input order: runs, keys, additive metrics (+ gene-bucket counts per tile)
   const int64_t tiles = cdiv(n, kTile);
@@ -406,17 +405,15 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     }
   }
   if (gene) {
-    // 4. gene view: bucket offsets, payload emission (input order), bucket reduction
-    uint32_t* goff = at<uint32_t>(ws, L.goffsets);
-    rc = scan_counts(gcounts, L.n_buckets * tiles, goff, at<uint64_t>(ws, L.gsums), s);
-    if (rc) return rc;
+    // 4. gene view: bucket starts, payload emission (input order), bucket reduction
+    uint32_t* gcur = at<uint32_t>(ws, L.gcursor);
     int64_t* gwork = at<int64_t>(ws, L.gwork);
     int64_t* n_gwork = at<int64_t>(ws, L.scalars) + 4;
     GenePayload* gpay = at<GenePayload>(ws, L.gpay);
-    LAUNCH("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), s, (const uint32_t*)goff, tiles, L.n_buckets, n, gwork,
+    LAUNCH("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), s, (const uint32_t*)gcounts, L.n_buckets, gcur, gwork,
            n_gwork);
-    LAUNCH("gene_emit", k_gene_emit, tgrid, dim3(kBlock), s, rec->gene, rc2, (const uint16_t*)dflags, n,
-           (const uint32_t*)goff, L.n_buckets, gpay);
+    LAUNCH("gene_emit", k_gene_emit, dim3((unsigned)cdiv(n, kEmitTile)), dim3(kBlock), s, rec->gene, rc2,
+           (const uint16_t*)dflags, n, gcur, L.n_buckets, gpay);
     HIPCHK(hipMemsetAsync(gene_partials, 0, sizeof(int64_t) * SCT_NP * (size_t)plan->n_gene_ids, s));
     LAUNCH("gene_reduce", k_gene_reduce, dim3((unsigned)L.max_gene_work), dim3(kBlock), s, (const GenePayload*)gpay,
            (const int64_t*)gwork, (const int64_t*)n_gwork, plan->n_gene_ids, gene_partials);

@@ -203,8 +203,8 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
   wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
   if (kGene) {
     __syncthreads();
-    const int64_t tiles = gridDim.x;
-    for (int i = t; i < n_buckets; i += kBlock) gene_counts[(int64_t)i * tiles + blockIdx.x] = s_hist[i];
+    for (int i = t; i < n_buckets; i += kBlock)
+      if (s_hist[i]) atomicAdd(&gene_counts[i], s_hist[i]);
   }
 }
 
@@ -219,9 +219,11 @@ __global__ void __launch_bounds__(kBlock) k_stream_sums(const int32_t* __restric
   __shared__ int32_t s_e[kTile];
   __shared__ int32_t s_prev;
   __shared__ uint64_t s_scan[kWaves + 1];
+  __shared__ double s_rcp[kRcpN];
   const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * kTile;
   const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
+  fill_rcp(s_rcp);  // visible after tile_run_ids' barriers
   tile_run_ids(ent, n, base, tile_n, tile_off[blockIdx.x], s_e, &s_prev, s_scan, nullptr);
 
   const int q0 = t * kItems;
@@ -284,7 +286,7 @@ __global__ void __launch_bounds__(kBlock) k_stream_sums(const int32_t* __restric
       cur_e = e;
       const uint32_t a = wide ? (wn[j / 2] >> (16 * (j % 2))) & 0xffffu : (wn[j / 4] >> (8 * (j % 4))) & 0xffu;
       const uint32_t d = wide ? (wd[j / 2] >> (16 * (j % 2))) & 0xffffu : (wd[j / 4] >> (8 * (j % 4))) & 0xffu;
-      fx_accumulate(lanes, ratio(a, d));
+      fx_accumulate(lanes, ratio_rcp(a, d, s_rcp));
     }
     wave_flush<kStreamLanes>(lanes, cur_e >= 0, cur_e, partials, slot);
   }

@@ -198,6 +198,24 @@ __device__ __forceinline__ uint32_t block_exclusive_max_n(uint32_t v, uint32_t* 
 // 0 for b == 0 (only reached by records the reference never aggregates)
 __device__ __forceinline__ double ratio(uint32_t a, uint32_t b) { return b ? (double)a / (double)b : 0.0; }
 
+// The same RN(a / b) without a division instruction sequence (the f64 divide is ~10 dependent
+// ops including v_rcp_f64 / v_div_scale / v_div_fixup, and dominated the quality streams):
+// with y = RN(1/b) from a table, q0 = RN(a*y), the residual r = a - q0*b is exact (one FMA),
+// and q = RN(q0 + r*y) is the correctly rounded quotient.  Checked bit-identical to IEEE a / b
+// for every a, b < 2^16 (tests/native/divcheck.c), which covers all uint8 / uint16 columns.
+constexpr int kRcpN = 256;  // table of 1/b for b < kRcpN (LDS); larger b divide once
+__device__ __forceinline__ void fill_rcp(double* s_rcp) {
+  for (int i = threadIdx.x; i < kRcpN; i += blockDim.x) s_rcp[i] = i ? 1.0 / (double)i : 0.0;
+}
+__device__ __forceinline__ double ratio_rcp(uint32_t a, uint32_t b, const double* s_rcp) {
+  if (b == 0) return 0.0;
+  const double y = b < (uint32_t)kRcpN ? s_rcp[b] : 1.0 / (double)b;
+  const double da = (double)a, db = (double)b;
+  const double q0 = da * y;
+  const double r = __fma_rn(-q0, db, da);
+  return __fma_rn(r, y, q0);
+}
+
 __device__ __forceinline__ uint32_t frag_hash(int32_t ref, int32_t pos, uint32_t strand) {
   uint32_t h = (uint32_t)ref * 0x9E3779B1u ^ ((uint32_t)pos * 0x85EBCA77u) ^ (strand * 0xC2B2AE3Du);
   h ^= h >> 15;

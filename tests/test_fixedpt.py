@@ -96,3 +96,14 @@ def test_partials_add(fx):
     fx.fx_finalize_lanes(tot.ctypes.data, 3000, ctypes.byref(m), ctypes.byref(v))
     em, ev = exact(xs)
     assert m.value == em and v.value == ev
+
+
+def test_division_free_quotient_is_exact():
+    """ratio_rcp (csrc/util.h) == IEEE a / b for every a, b < 2^16 (exhaustive, ~4.3e9 pairs)."""
+    exe = os.path.join(HERE, "native", "divcheck")
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", "-o", exe,
+                    os.path.join(HERE, "native", "divcheck.c"), "-lm"], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    tot, bad = (int(v) for v in out.stdout.split())
+    assert tot == 65535 * 65536
+    assert bad == 0 and out.returncode == 0
