@@ -55,7 +55,18 @@ constexpr int kHTBits = 11;
 constexpr int kHTSlots = 1 << kHTBits;      // hash table slots: > kTileCap, so probing ends
 constexpr int kWinBits = 10;                // bucket ordinal (window offset) bits in the keys
 constexpr int kNarrowK1Bits = 32 - 2 - kWinBits;  // k1 ids up to 20 bits use a 32-bit k1 table
+// big buckets: kBCap < records <= kBigCap, one kBigBlock-thread block each with kBigSlots-slot
+// tables (load factor <= 3/4).  Typically a hot gene's records in one cell: taking them here
+// instead of splitting them further on the umi bits saves whole partition levels.
+#ifndef SCT_BIG_BLOCK
+#define SCT_BIG_BLOCK 1024
+#endif
+constexpr int kBigBlock = SCT_BIG_BLOCK;
+constexpr int kBigBits = 12;
+constexpr int kBigSlots = 1 << kBigBits;
+constexpr int kBigCap = 3 * kBigSlots / 4 - 1;  // 3071
 static_assert(kTileCap < kHTSlots, "a tile's keys always fit its tables");
+static_assert(kBigCap < kBigSlots && kBigSlots <= 4096, "big-bucket keys fit its tables; 12-bit slots");
 static_assert(kWin == 2 * kHBlock && (1 << kWinBits) == kWin, "window layout");
 static_assert(kBCap < (1 << 11), "count field");
 static_assert(kHTSlots <= 4096, "molecule slots are 12 bits in the fragment key");
@@ -76,8 +87,9 @@ struct Seg {
 struct Work {
   uint32_t seg, chunk;
 };
-struct BucketCtl {  // device counters of one level (n_giant accumulates over levels)
+struct BucketCtl {  // device counters of one level (n_giant, n_big accumulate over levels)
   uint32_t n_seg, n_work, n_giant, err;  // err: a mapped ref id >= 2^kRefBits (set by build_keys)
+  uint32_t n_big;
 };
 
 __device__ __forceinline__ uint64_t payload_w0(uint64_t key, int32_t ref, bool reverse, bool mapped, bool mito) {
@@ -96,10 +108,10 @@ __device__ __forceinline__ void push_segment(const Seg& sg, Seg* __restrict__ se
   for (uint32_t k = 0; k < nw; k++) work[w0 + k] = Work{id, k};
 }
 
-// level 0: small entities are terminal buckets; larger ones become segments
+// level 0: small entities are terminal buckets, mid-sized ones big buckets; larger ones segments
 __global__ void k_bucket_level0(const int64_t* __restrict__ ent_start, int64_t n_ent, int64_t n,
                                 uint16_t* __restrict__ bdesc, uint32_t* __restrict__ bent, Seg* __restrict__ seg,
-                                Work* __restrict__ work, BucketCtl* ctl) {
+                                Work* __restrict__ work, Seg* __restrict__ bigs, BucketCtl* ctl) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n_ent) return;
   const int64_t s0 = ent_start[e];
@@ -108,6 +120,10 @@ __global__ void k_bucket_level0(const int64_t* __restrict__ ent_start, int64_t n
   if (c <= (uint32_t)kBCap) {
     bdesc[s0] = (uint16_t)c;
     bent[s0] = (uint32_t)e;
+    return;
+  }
+  if (c <= (uint32_t)kBigCap) {
+    bigs[atomicAdd(&ctl->n_big, 1u)] = Seg{(uint32_t)s0, c, (uint32_t)e, 0u};
     return;
   }
   push_segment(Seg{(uint32_t)s0, c, (uint32_t)e, 0u}, seg, work, ctl);
@@ -272,7 +288,7 @@ __device__ __forceinline__ uint32_t split_flags(int Kb, int depth, int depth1, i
 
 // One block per segment, one thread per child digit: the children's record ranges (an exclusive
 // scan of the digit counts; the scatter's cursors) and their classification -- terminal
-// bucket, giant, or next-level segment.  The block's new segments and work items are reserved
+// bucket, big bucket, giant, or next-level segment.  The block's new segments and work items are reserved
 // with one atomic each.
 __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restrict__ seg,
                                                             const uint32_t* __restrict__ hist,
@@ -280,7 +296,8 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
                                                             int K1, int KM, int KB, int parity,
                                                             uint16_t* __restrict__ bdesc, uint32_t* __restrict__ bent,
                                                             Seg* __restrict__ nseg, Work* __restrict__ nwork,
-                                                            Seg* __restrict__ giants, BucketCtl* ctl) {
+                                                            Seg* __restrict__ giants, Seg* __restrict__ bigs,
+                                                            BucketCtl* ctl) {
   __shared__ uint32_t s_c[kRadix];
   __shared__ uint64_t s_scan[kWaves + 1];
   __shared__ uint32_t s_base[2];
@@ -300,14 +317,17 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
   }
   const uint32_t par = parity ? BD_PARITY : 0u;
   const bool terminal = c && c <= (uint32_t)kBCap;
-  const bool giant = c > (uint32_t)kBCap && depth1 >= KB;
-  const bool push = c > (uint32_t)kBCap && !giant;
+  const bool big = c > (uint32_t)kBCap && c <= (uint32_t)kBigCap;
+  const bool giant = c > (uint32_t)kBigCap && depth1 >= KB;
+  const bool push = c > (uint32_t)kBigCap && !giant;
   if (terminal) {
     bdesc[start] = (uint16_t)(c | fl | par);
     bent[start] = sg.ent;
   } else if (giant) {
     const uint32_t id = atomicAdd(&ctl->n_giant, 1u);
     giants[id] = Seg{start, c, sg.ent, fl | par};
+  } else if (big) {
+    bigs[atomicAdd(&ctl->n_big, 1u)] = Seg{start, c, sg.ent, fl | par};
   }
   const uint32_t nw = push ? (c + kChunk - 1) / kChunk : 0u;
   uint64_t tot_s, tot_w;
@@ -326,17 +346,18 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
 }
 
 // ---- LDS hash tables: entries key << 2 | state, state bit 0 = present, bit 1 = seen twice ----
-__device__ __forceinline__ uint32_t ht_home(unsigned long long key) {
-  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - kHTBits));
+__device__ __forceinline__ uint32_t ht_home(unsigned long long key, int tb) {
+  return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - tb));
 }
-__device__ __forceinline__ uint32_t ht_home(unsigned int key) { return (key * 0x9E3779B1u) >> (32 - kHTBits); }
+__device__ __forceinline__ uint32_t ht_home(unsigned int key, int tb) { return (key * 0x9E3779B1u) >> (32 - tb); }
 
-// Insert `key` (low two bits zero).  Returns the key's slot; ev = 1 for the record that inserted
-// the key (its head), 2 for the first record that found it present, else 0.  The table has
-// more slots than a tile has records, so the probe always ends.
+// Insert `key` (low two bits zero) into a table of 2^tb slots.  Returns the key's slot; ev = 1
+// for the record that inserted the key (its head), 2 for the first record that found it
+// present, else 0.  The table has more slots than the block has records, so the probe ends.
 template <typename E>
-__device__ __forceinline__ uint32_t ht_insert(E* T, E key, int& ev) {
-  uint32_t h = ht_home(key);
+__device__ __forceinline__ uint32_t ht_insert(E* T, E key, int& ev, int tb = kHTBits) {
+  const uint32_t mask = (1u << tb) - 1;
+  uint32_t h = ht_home(key, tb);
   while (true) {
     const E old = atomicCAS(&T[h], (E)0, (E)(key | 1));
     if (old == 0) {
@@ -348,7 +369,7 @@ __device__ __forceinline__ uint32_t ht_insert(E* T, E key, int& ev) {
       if (!(old & 2) && !(atomicOr(&T[h], (E)2) & 2)) ev = 2;
       return h;
     }
-    h = (h + 1) & (kHTSlots - 1);
+    h = (h + 1) & mask;
   }
 }
 
@@ -462,6 +483,90 @@ __global__ void __launch_bounds__(kHBlock) k_hash_tile(const uint16_t* __restric
     }
   }
   wave_flush<kDistinct>(acc, cur_e >= 0, cur_e, partials, slot);
+}
+
+// One big bucket (kBCap < records <= kBigCap, bucket.h header) per block: the hash tile's
+// per-record logic with one bucket per block and kBigSlots-slot tables.
+template <bool kCell, bool kGene, bool kWideK1>
+__global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict__ bigs,
+                                                          const uint64_t* __restrict__ w0_a,
+                                                          const uint64_t* __restrict__ w1_a,
+                                                          const uint64_t* __restrict__ w0_b,
+                                                          const uint64_t* __restrict__ w1_b, Bits b,
+                                                          int64_t* __restrict__ partials,
+                                                          uint16_t* __restrict__ dflags) {
+  using K1E = typename std::conditional<kWideK1, unsigned long long, unsigned int>::type;
+  __shared__ K1E s_k1[kBigSlots];
+  __shared__ unsigned long long s_mol[kBigSlots];
+  __shared__ unsigned long long s_frg[kBigSlots];
+  __shared__ int32_t s_acc[kDistinct];
+  const int t = threadIdx.x;
+  const Seg g = bigs[blockIdx.x];
+  int tb = kHTBits;  // tables sized to the bucket: load factor <= 3/4
+  while ((1u << tb) * 3u < 4u * g.cnt + 4u) tb++;
+  const int slots = 1 << tb;
+  {
+    uint4* z = reinterpret_cast<uint4*>(s_mol);
+    for (int i = t; i < slots / 2; i += kBigBlock) z[i] = make_uint4(0, 0, 0, 0);
+    z = reinterpret_cast<uint4*>(s_frg);
+    for (int i = t; i < slots / 2; i += kBigBlock) z[i] = make_uint4(0, 0, 0, 0);
+    z = reinterpret_cast<uint4*>(s_k1);
+    for (int i = t; i < (int)(slots * sizeof(K1E) / 16); i += kBigBlock) z[i] = make_uint4(0, 0, 0, 0);
+    if (t < kDistinct) s_acc[t] = 0;
+  }
+  __syncthreads();
+  const uint32_t bd = g.flags;
+  const bool pb = bd & BD_PARITY;
+  const uint64_t* W0 = pb ? w0_b : w0_a;
+  const uint64_t* W1 = pb ? w1_b : w1_a;
+  const int KB = b.k1 + b.k2 + b.h;
+  const uint64_t kmask = (1ull << KB) - 1;
+  const int sh_mol = b.h, sh_k1 = b.k2 + b.h;
+  int32_t acc[kDistinct];
+#pragma unroll
+  for (int i = 0; i < kDistinct; i++) acc[i] = 0;
+  for (uint32_t p = t; p < g.cnt; p += kBigBlock) {
+    const uint64_t x0 = W0[g.start + p];
+    const uint64_t x1 = W1[g.start + p];
+    const uint64_t key = (x0 >> kKeyShift) & kmask;
+    int ek, em, ef = 0;
+    ht_insert<K1E>(s_k1, (K1E)((key >> sh_k1) << 2), ek, tb);
+    const uint32_t ms = ht_insert<unsigned long long>(s_mol, (key >> sh_mol) << 2, em, tb);
+    if (x0 & kW0Mapped) {
+      const uint64_t fk = ((((uint64_t)ms << 18) | payload_frag(x0)) << 32) | (uint32_t)x1;
+      ht_insert<unsigned long long>(s_frg, fk << 2, ef, tb);
+    }
+    const bool k1_head = ek == 1 && !(bd & BD_K1_NOHEAD);
+    const bool k1_multi = (bd & BD_K1_MULTI) ? k1_head : ek == 2;
+    const bool mol_head = em == 1 && !(bd & BD_MOL_NOHEAD);
+    const bool mol_second = (bd & BD_MOL_MULTI) ? mol_head : em == 2;
+    acc[0] += mol_head;
+    acc[1] += (int32_t)mol_head - (int32_t)mol_second;
+    acc[2] += ef == 1;
+    acc[3] += (int32_t)(ef == 1) - (int32_t)(ef == 2);
+    acc[4] += k1_head;
+    acc[5] += k1_multi;
+    if constexpr (kCell) acc[6] += (k1_head && (x0 & kW0Mito)) ? 1 : 0;
+    if constexpr (kGene) {
+      const uint16_t f = (mol_head ? (DF_MOL_HEAD | DF_MOL_SINGLE) : 0) | (mol_second ? DF_MOL_SECOND : 0) |
+                         (ef == 1 ? (DF_FRAG_FIRST | DF_FRAG_SINGLE) : 0) | (ef == 2 ? DF_FRAG_SECOND : 0) |
+                         (k1_head ? DF_K1_HEAD : 0) | (k1_multi ? DF_K1_MULTI : 0);
+      dflags[x1 >> 32] = f;
+    }
+  }
+  // one entity per block: wave sums, then one LDS add per wave and lane, then the row
+  const int lane = t & (kWave - 1);
+  int32_t mine = 0;
+#pragma unroll
+  for (int i = 0; i < kDistinct; i++) {
+    const int32_t tot = wave_sum_dpp(acc[i]);
+    mine = lane == i ? tot : mine;
+  }
+  if (lane < kDistinct && mine) atomicAdd(&s_acc[lane], mine);
+  __syncthreads();
+  if (t < kDistinct && s_acc[t])
+    atomicAdd((unsigned long long*)&partials[(int64_t)g.ent * SCT_NP + distinct_slot(t)],
+              (unsigned long long)(int64_t)s_acc[t]);
 }
 
 // A bucket whose whole key' is fixed and still holds > kBCap records: one piece of one

@@ -40,7 +40,7 @@ namespace {
 struct Layout {
   size_t tile_cnt, scalars, scan_sums, keys_a, keys_b, vals_a, vals_b, counts, offsets, ent_start, partials;
   size_t gcounts, gcursor, gwork, dflags, gpay, seen, zero_mito;
-  size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, total;
+  size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, bigs, total;
   int64_t num_tiles, num_chunks, max_ent, max_gene_work, max_seg, max_work;
   int n_buckets;
   bool gene;
@@ -94,6 +94,7 @@ Layout layout_for(const sct_plan_t* plan) {
   L.seg_hist = take(sizeof(uint32_t) * kRadix * (size_t)L.max_seg);
   L.seg_cur = take(sizeof(uint32_t) * kRadix * (size_t)L.max_seg);
   L.giants = take(sizeof(Seg) * (size_t)L.max_seg);
+  L.bigs = take(sizeof(Seg) * (size_t)L.max_seg);
   L.total = off;
   return L;
 }
@@ -195,9 +196,11 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   BucketCtl* ctl = bucket_ctl(ws, L);
   const int KB = b.k1 + b.k2 + b.h;
   HIPCHK(hipMemsetAsync(bdesc, 0, sizeof(uint16_t) * (size_t)n, s));
+  Seg* bigs = at<Seg>(ws, L.bigs);
   HIPCHK(hipMemsetAsync(ctl, 0, 3 * sizeof(uint32_t), s));  // keeps ctl->err from build_keys
+  HIPCHK(hipMemsetAsync(&ctl->n_big, 0, sizeof(uint32_t), s));
   LAUNCH("bucket_level0", k_bucket_level0, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, ent_start, n_ent, n,
-         bdesc, bent, seg[0], work[0], ctl);
+         bdesc, bent, seg[0], work[0], bigs, ctl);
   BucketCtl h{};
   HIPCHK(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -220,7 +223,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), s));  // next level's n_seg, n_work
     LAUNCH("bucket_classify", k_bucket_classify, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c],
            (const uint32_t*)hist, cur, depth, bits, b.k1, b.k1 + b.k2, KB, level & 1, bdesc, bent, seg[c ^ 1],
-           work[c ^ 1], giants, ctl);
+           work[c ^ 1], giants, bigs, ctl);
     LAUNCH("bucket_scatter", k_bucket_scatter, dim3(h.n_work), dim3(kBlock), s, kin, vin, kout, vout,
            (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
     HIPCHK(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
@@ -237,6 +240,21 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     rc = launch_hash_tile<false>(cell, gene, tgrid, s, bdesc, bent, ka, va, kb, vb, n, b, partials, dflags);
   }
   if (rc) return rc;
+  if (h.n_big > 0) {
+    const dim3 bgrid(h.n_big);
+    const bool wide = b.k1 > kNarrowK1Bits;
+#define SCT_BIG(C, G, W)                                                                                          \
+  LAUNCH("big_bucket", (k_big_bucket<C, G, W>), bgrid, dim3(kBigBlock), s, (const Seg*)bigs, ka, va, kb, vb, b, \
+         partials, dflags)
+    if (cell && gene) {
+      if (wide) { SCT_BIG(true, true, true); } else { SCT_BIG(true, true, false); }
+    } else if (cell) {
+      if (wide) { SCT_BIG(true, false, true); } else { SCT_BIG(true, false, false); }
+    } else {
+      if (wide) { SCT_BIG(false, false, true); } else { SCT_BIG(false, false, false); }
+    }
+#undef SCT_BIG
+  }
   if (h.n_giant > 0) {
     const dim3 ggrid(h.n_giant);
     if (cell && gene) {
