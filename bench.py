@@ -36,8 +36,8 @@ ALG_BYTES = {
     "hash_tile": 20,         # read payload w0 + w1 (16) + bucket descriptor (2), write dflags (2)
     "bucket_scatter": 32,    # read payload 16, write payload 16 (records of the level's segments)
     "bucket_hist": 8,        # read w0
-    "build_keys": 38,        # read cell/gene/umi/ref/pos (20) + bits/xf (2), write payload (16)
-    "stream_sums": 14,       # read entity column (4) + uy/gq/cy quality columns (10)
+    "build_keys": 48,        # read cell/gene/umi/ref/pos (20) + bits/xf (2) + uy/gq/cy (10), write payload (16)
+    "big_bucket": 18,        # read payload w0 + w1 (16) of the big buckets' records, write dflags (2)
     "gene_emit": 32,         # read gene/bits/xf/dflags/uy/gq (16), write 16-byte gene payload
     "gene_reduce": 16,       # read the 16-byte gene payload
     "radix_downsweep": 24,   # global-sort path: read key 8 + value 4, write key 8 + value 4

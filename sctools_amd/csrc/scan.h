@@ -39,6 +39,28 @@ __global__ void k_scan_small(uint64_t* __restrict__ data, int64_t m, uint64_t* _
   if (threadIdx.x == 0 && out_total) *out_total = carry;
 }
 
+// one 1024-thread block: exclusive scan of m uint64 in place, each thread owning a contiguous
+// run of elements (a few tens of microseconds faster than k_scan_small's 256-wide sweeps at
+// ~25K elements); the total goes to *out_total (if set)
+constexpr int kScanWide = 1024;
+__global__ void __launch_bounds__(kScanWide) k_scan_wide(uint64_t* __restrict__ data, int64_t m,
+                                                         uint64_t* __restrict__ out_total) {
+  __shared__ uint64_t lds[kScanWide / kWave + 1];
+  const int64_t per = (m + kScanWide - 1) / kScanWide;
+  const int64_t b = (int64_t)threadIdx.x * per;
+  const int64_t e = b + per < m ? b + per : m;
+  uint64_t s = 0;
+  for (int64_t i = b; i < e; i++) s += data[i];
+  uint64_t tot;
+  uint64_t run = block_exclusive_scan_n<kScanWide, uint64_t>(s, &tot, lds);
+  for (int64_t i = b; i < e; i++) {
+    const uint64_t v = data[i];
+    data[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0 && out_total) *out_total = tot;
+}
+
 __global__ void k_scan_apply(const uint32_t* __restrict__ in, int64_t m, const uint64_t* __restrict__ block_off,
                              uint32_t* __restrict__ out) {
   __shared__ uint64_t lds[kWaves + 1];

@@ -148,7 +148,7 @@ int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool du
   }
   HIPCHK(hipMemsetAsync(sc, 0, 2 * sizeof(uint64_t), s));
   LAUNCH("heads", k_heads, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, sc + 1);
-  LAUNCH("scan", k_scan_small, dim3(1), dim3(kBlock), s, tc, tiles, sc);
+  LAUNCH("scan", k_scan_wide, dim3(1), dim3(kScanWide), s, tc, tiles, sc);
   uint64_t host[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(host, sc, sizeof(host), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -274,20 +274,20 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
 // The RUN-mode pipeline (entity = runs of the cell column, or of the gene column in gene
 // mode; GROUPED runs the cell view).  Writes partial rows into the workspace, output rows
 // if out_i / out_f are set, and grouped gene partials (cell view) if gene_partials is set.
-template <bool kBucket>
+template <bool kBucket, bool kStreams>
 int launch_build_keys(bool cell, bool gene, dim3 grid, hipStream_t s, const KeyCols& kc, const RecCols& rc2,
                       const uint8_t* mito, int64_t n, const uint64_t* toff, const Bits& b, uint64_t* keys,
                       void* vals, int64_t* ent_start, int64_t* partials, uint32_t* gcounts, int n_buckets,
                       uint32_t* err) {
   if (cell && gene) {
-    LAUNCH("build_keys", (k_build_keys_run<true, true, kBucket>), grid, dim3(kBlock), s, kc, rc2, mito, n, toff, b,
-           keys, vals, ent_start, partials, gcounts, n_buckets, err);
+    LAUNCH("build_keys", (k_build_keys_run<true, true, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito, n,
+           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err);
   } else if (cell) {
-    LAUNCH("build_keys", (k_build_keys_run<true, false, kBucket>), grid, dim3(kBlock), s, kc, rc2, mito, n, toff, b,
-           keys, vals, ent_start, partials, gcounts, n_buckets, err);
+    LAUNCH("build_keys", (k_build_keys_run<true, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito, n,
+           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err);
   } else {
-    LAUNCH("build_keys", (k_build_keys_run<false, false, kBucket>), grid, dim3(kBlock), s, kc, rc2, mito, n, toff,
-           b, keys, vals, ent_start, partials, gcounts, n_buckets, err);
+    LAUNCH("build_keys", (k_build_keys_run<false, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito,
+           n, toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err);
   }
   return SCT_OK;
 }
@@ -364,23 +364,23 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   const int64_t tiles = cdiv(n, kTile);
   const dim3 tgrid((unsigned)tiles);
   const uint64_t* toff = at<uint64_t>(ws, L.tile_cnt);
+  // exact mean / variance lanes of the output rows ride along in the same launch
+  const bool streams = exact && out_i;
   if (bucket) {
     BucketCtl* ctl = bucket_ctl(ws, L);
     HIPCHK(hipMemsetAsync(ctl, 0, sizeof(BucketCtl), s));
-    rc = launch_build_keys<true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, at<uint64_t>(ws, L.vals_a),
-                                 ent_start, partials, gcounts, L.n_buckets, &ctl->err);
+    uint64_t* va = at<uint64_t>(ws, L.vals_a);
+    rc = streams ? launch_build_keys<true, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
+                                                 partials, gcounts, L.n_buckets, &ctl->err)
+                 : launch_build_keys<true, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
+                                                  partials, gcounts, L.n_buckets, &ctl->err);
   } else {
-    rc = launch_build_keys<false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va, ent_start, partials,
-                                  gcounts, L.n_buckets, nullptr);
+    rc = streams ? launch_build_keys<false, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
+                                                  ent_start, partials, gcounts, L.n_buckets, nullptr)
+                 : launch_build_keys<false, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
+                                                   ent_start, partials, gcounts, L.n_buckets, nullptr);
   }
   if (rc) return rc;
-  if (exact && out_i) {  // exact mean / variance lanes of the output rows
-    if (cell) {
-      LAUNCH("stream_sums", k_stream_sums<true>, tgrid, dim3(kBlock), s, ent_col, rc2, n, toff, partials);
-    } else {
-      LAUNCH("stream_sums", k_stream_sums<false>, tgrid, dim3(kBlock), s, ent_col, rc2, n, toff, partials);
-    }
-  }
 
   // 2-3. distinct counts (+ per-record distinct events for the gene view)
   uint16_t* dflags = gene ? at<uint16_t>(ws, L.dflags) : nullptr;

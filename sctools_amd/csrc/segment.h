@@ -121,111 +121,13 @@ __device__ __forceinline__ void tile_run_ids(const int32_t* __restrict__ ent, in
   __syncthreads();
 }
 
-// kBucket: write the bucket path's 16-byte payload (bucket.h: w0 = key' | ref | strand |
-// mapped, w1 = index | pos; a mapped ref id >= 2^kRefBits raises *err).  Otherwise the
-// global sort's (key with entity bits, u32 value with bit 31 = unmapped).
-template <bool kCell, bool kGene, bool kBucket>
-__global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r, const uint8_t* __restrict__ k1_is_mito,
-                                                           int64_t n, const uint64_t* __restrict__ tile_off, Bits b,
-                                                           uint64_t* __restrict__ keys, void* __restrict__ vals,
-                                                           int64_t* __restrict__ ent_start,
-                                                           int64_t* __restrict__ partials,
-                                                           uint32_t* __restrict__ gene_counts, int n_buckets,
-                                                           uint32_t* __restrict__ err) {
-  static_assert(!kGene || kCell, "gene buckets come from the cell view");
-  __shared__ int32_t s_e[kTile];
-  __shared__ int32_t s_prev;
-  __shared__ uint64_t s_scan[kWaves + 1];
-  __shared__ uint32_t s_hist[kGene ? kMaxGeneBuckets : 1];
-  const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kTile;
-  const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
-  if (kGene)
-    for (int i = t; i < n_buckets; i += kBlock) s_hist[i] = 0;
-  // 1-2. run index of every record of the tile
-  tile_run_ids(c.ent, n, base, tile_n, tile_off[blockIdx.x], s_e, &s_prev, s_scan, ent_start);
-
-  // 3. striped pass: keys, values and the run's additive metrics.  Runs are contiguous, so
-  // in a round the wave's lanes cross a run boundary together: flush wave-cooperatively.
-  using A = AddAcc<kCell>;
-  A acc;
-  acc.clear();
-  int64_t cur_e = -1;
-  const auto slot = [](int i) { return A::slot(i); };
-  for (int j = 0; j < kItems; j++) {
-    const int q = j * kBlock + t;
-    const bool valid = q < tile_n;
-    const int64_t p = base + q;
-    const int64_t e = valid ? (int64_t)s_e[q] : cur_e;
-    wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
-    if (!valid) continue;
-    cur_e = e;
-    const uint32_t k1 = (uint32_t)c.k1[p];
-    const uint32_t k2 = (uint32_t)c.k2[p];
-    const uint8_t bt = r.bits[p];
-    const uint8_t xf = r.xf[p];
-    const bool mapped = !(bt & SCT_B_UNMAPPED);
-    const int32_t ref = r.ref[p];
-    const int32_t pos = r.pos[p];
-    const bool rev = bt & SCT_B_REVERSE;
-    const uint32_t hsh = mapped ? frag_hash(ref, pos, rev ? 1u : 0u) : 0u;
-    if constexpr (kBucket) {
-      const bool mito = kCell ? k1_is_mito[k1] != 0 : false;
-      keys[p] = payload_w0(make_key(0, k1, k2, hsh, b), ref, rev, mapped, mito);
-      static_cast<uint64_t*>(vals)[p] = ((uint64_t)p << 32) | (uint32_t)pos;
-      if (mapped && (uint32_t)ref >= (1u << kRefBits)) atomicOr(err, 1u);
-    } else {
-      keys[p] = make_key((uint64_t)e, k1, k2, hsh, b);
-      static_cast<uint32_t*>(vals)[p] = (uint32_t)p | (mapped ? 0u : kUnmappedValBit);
-    }
-    // MetricAggregator.parse_molecule (aggregator.py:259-334)
-    acc.v[0] += 1;
-    acc.v[1] += (bt & SCT_B_PERFECT_UMI) ? 1 : 0;
-    if (mapped) {
-      const bool nh1 = bt & SCT_B_NH1;
-      acc.v[2] += (xf == SCT_XF_CODING);
-      acc.v[3] += (xf == SCT_XF_INTRONIC);
-      acc.v[4] += (xf == SCT_XF_UTR);
-      acc.v[5] += nh1 ? 1 : 0;
-      acc.v[6] += nh1 ? 0 : 1;
-      acc.v[7] += (bt & SCT_B_DUPLICATE) ? 1 : 0;
-      acc.v[8] += (bt & SCT_B_SPLICED) ? 1 : 0;
-    }
-    if constexpr (kCell) {
-      // CellMetrics.parse_extra_fields (aggregator.py:507-530) + mito reads (463-490)
-      acc.v[9] += ((bt & SCT_B_HAS_CB) && (bt & SCT_B_PERFECT_CB)) ? 1 : 0;
-      acc.v[10] += (xf == SCT_XF_INTERGENIC);
-      acc.v[11] += (xf == SCT_XF_ABSENT);
-      acc.v[12] += k1_is_mito[k1];
-    }
-    if (kGene) atomicAdd(&s_hist[k1 / kGenesPerBucket], 1u);
-  }
-  wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
-  if (kGene) {
-    __syncthreads();
-    for (int i = t; i < n_buckets; i += kBlock)
-      if (s_hist[i]) atomicAdd(&gene_counts[i], s_hist[i]);
-  }
-}
-
-// Exact fixed-point lanes of the quality streams (fixedpt.h), one run at a time, in input
-// order: UY fraction, genomic fraction, genomic mean quality (aggregator.py:266-292) and,
-// for cells, the CY fraction (aggregator.py:507-514).  Blocked items with 16-byte vector
+// The exact fixed-point lanes of the quality streams for one tile whose run ids are in s_e
+// (tile_run_ids): blocked items (kItems consecutive records per thread) with 16-byte vector
 // loads; the streams are summed one after another so only 8 lanes are live per thread.
 template <bool kCell>
-__global__ void __launch_bounds__(kBlock) k_stream_sums(const int32_t* __restrict__ ent, RecCols r, int64_t n,
-                                                        const uint64_t* __restrict__ tile_off,
-                                                        int64_t* __restrict__ partials) {
-  __shared__ int32_t s_e[kTile];
-  __shared__ int32_t s_prev;
-  __shared__ uint64_t s_scan[kWaves + 1];
-  __shared__ double s_rcp[kRcpN];
+__device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int tile_n, const int32_t* s_e,
+                                            const double* s_rcp, int64_t* __restrict__ partials) {
   const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kTile;
-  const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
-  fill_rcp(s_rcp);  // visible after tile_run_ids' barriers
-  tile_run_ids(ent, n, base, tile_n, tile_off[blockIdx.x], s_e, &s_prev, s_scan, nullptr);
-
   const int q0 = t * kItems;
   const int64_t p0 = base + q0;
   const bool full = q0 + kItems <= tile_n;
@@ -290,6 +192,98 @@ __global__ void __launch_bounds__(kBlock) k_stream_sums(const int32_t* __restric
     }
     wave_flush<kStreamLanes>(lanes, cur_e >= 0, cur_e, partials, slot);
   }
+}
+
+// kBucket: write the bucket path's 16-byte payload (bucket.h: w0 = key' | ref | strand |
+// mapped, w1 = index | pos; a mapped ref id >= 2^kRefBits raises *err).  Otherwise the
+// global sort's (key with entity bits, u32 value with bit 31 = unmapped).
+// kStreams: also the exact quality-stream lanes of the runs (stream_tile), reusing the tile's
+// run ids: the stream ALU work overlaps the key pass's memory traffic in one launch.
+template <bool kCell, bool kGene, bool kBucket, bool kStreams>
+__global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r, const uint8_t* __restrict__ k1_is_mito,
+                                                           int64_t n, const uint64_t* __restrict__ tile_off, Bits b,
+                                                           uint64_t* __restrict__ keys, void* __restrict__ vals,
+                                                           int64_t* __restrict__ ent_start,
+                                                           int64_t* __restrict__ partials,
+                                                           uint32_t* __restrict__ gene_counts, int n_buckets,
+                                                           uint32_t* __restrict__ err) {
+  static_assert(!kGene || kCell, "gene buckets come from the cell view");
+  __shared__ int32_t s_e[kTile];
+  __shared__ int32_t s_prev;
+  __shared__ uint64_t s_scan[kWaves + 1];
+  __shared__ uint32_t s_hist[kGene ? kMaxGeneBuckets : 1];
+  __shared__ double s_rcp[kStreams ? kRcpN : 1];
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
+  if (kGene)
+    for (int i = t; i < n_buckets; i += kBlock) s_hist[i] = 0;
+  if (kStreams) fill_rcp(s_rcp);  // visible after tile_run_ids' barriers
+  // 1-2. run index of every record of the tile
+  tile_run_ids(c.ent, n, base, tile_n, tile_off[blockIdx.x], s_e, &s_prev, s_scan, ent_start);
+
+  // 3. striped pass: keys, values and the run's additive metrics.  Runs are contiguous, so
+  // in a round the wave's lanes cross a run boundary together: flush wave-cooperatively.
+  using A = AddAcc<kCell>;
+  A acc;
+  acc.clear();
+  int64_t cur_e = -1;
+  const auto slot = [](int i) { return A::slot(i); };
+  for (int j = 0; j < kItems; j++) {
+    const int q = j * kBlock + t;
+    const bool valid = q < tile_n;
+    const int64_t p = base + q;
+    const int64_t e = valid ? (int64_t)s_e[q] : cur_e;
+    wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
+    if (!valid) continue;
+    cur_e = e;
+    const uint32_t k1 = (uint32_t)c.k1[p];
+    const uint32_t k2 = (uint32_t)c.k2[p];
+    const uint8_t bt = r.bits[p];
+    const uint8_t xf = r.xf[p];
+    const bool mapped = !(bt & SCT_B_UNMAPPED);
+    const int32_t ref = r.ref[p];
+    const int32_t pos = r.pos[p];
+    const bool rev = bt & SCT_B_REVERSE;
+    const uint32_t hsh = mapped ? frag_hash(ref, pos, rev ? 1u : 0u) : 0u;
+    if constexpr (kBucket) {
+      const bool mito = kCell ? k1_is_mito[k1] != 0 : false;
+      keys[p] = payload_w0(make_key(0, k1, k2, hsh, b), ref, rev, mapped, mito);
+      static_cast<uint64_t*>(vals)[p] = ((uint64_t)p << 32) | (uint32_t)pos;
+      if (mapped && (uint32_t)ref >= (1u << kRefBits)) atomicOr(err, 1u);
+    } else {
+      keys[p] = make_key((uint64_t)e, k1, k2, hsh, b);
+      static_cast<uint32_t*>(vals)[p] = (uint32_t)p | (mapped ? 0u : kUnmappedValBit);
+    }
+    // MetricAggregator.parse_molecule (aggregator.py:259-334)
+    acc.v[0] += 1;
+    acc.v[1] += (bt & SCT_B_PERFECT_UMI) ? 1 : 0;
+    if (mapped) {
+      const bool nh1 = bt & SCT_B_NH1;
+      acc.v[2] += (xf == SCT_XF_CODING);
+      acc.v[3] += (xf == SCT_XF_INTRONIC);
+      acc.v[4] += (xf == SCT_XF_UTR);
+      acc.v[5] += nh1 ? 1 : 0;
+      acc.v[6] += nh1 ? 0 : 1;
+      acc.v[7] += (bt & SCT_B_DUPLICATE) ? 1 : 0;
+      acc.v[8] += (bt & SCT_B_SPLICED) ? 1 : 0;
+    }
+    if constexpr (kCell) {
+      // CellMetrics.parse_extra_fields (aggregator.py:507-530) + mito reads (463-490)
+      acc.v[9] += ((bt & SCT_B_HAS_CB) && (bt & SCT_B_PERFECT_CB)) ? 1 : 0;
+      acc.v[10] += (xf == SCT_XF_INTERGENIC);
+      acc.v[11] += (xf == SCT_XF_ABSENT);
+      acc.v[12] += k1_is_mito[k1];
+    }
+    if (kGene) atomicAdd(&s_hist[k1 / kGenesPerBucket], 1u);
+  }
+  wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
+  if (kGene) {
+    __syncthreads();
+    for (int i = t; i < n_buckets; i += kBlock)
+      if (s_hist[i]) atomicAdd(&gene_counts[i], s_hist[i]);
+  }
+  if constexpr (kStreams) stream_tile<kCell>(r, base, tile_n, s_e, s_rcp, partials);
 }
 
 }  // namespace sct
