@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="target seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"),
+                    help="rocprofv3 --pmc per-kernel HBM bytes (tools/pmc_passes.sh) for roofline.traffic")
     return ap.parse_args()
 
 
@@ -111,6 +113,8 @@ def main():
     host_genei = torch.empty((data.n_gene_ids, 24), dtype=torch.int64, pin_memory=True)
     host_genef = torch.empty((data.n_gene_ids, 12), dtype=torch.float64, pin_memory=True)
 
+    copy_stream = torch.cuda.Stream(device=dev)
+
     def step():
         if args.float_mode == "exact":
             # one pass: cell rows + grouped gene partials share the cell-view sort
@@ -120,10 +124,13 @@ def main():
             eng.gene_partials(data.cols, dims, out=partials)
         D.allreduce_partials(partials)  # RCCL over xGMI when N > 1; no-op at N = 1
         gi, gf = eng.finalize_partials(partials)
-        host_cells[: ci.shape[0]].copy_(ci, non_blocking=True)
-        host_cellf[: cf.shape[0]].copy_(cf, non_blocking=True)
-        host_genei.copy_(gi, non_blocking=True)
-        host_genef.copy_(gf, non_blocking=True)
+        # rows -> pinned host on a copy stream: this step's D2H overlaps the next step's kernels
+        copy_stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(copy_stream):
+            for src, dst in ((ci, host_cells[: ci.shape[0]]), (cf, host_cellf[: cf.shape[0]]), (gi, host_genei),
+                             (gf, host_genef)):
+                src.record_stream(copy_stream)
+                dst.copy_(src, non_blocking=True)
         return ci.shape[0]
 
     for _ in range(args.warmup):
@@ -169,6 +176,7 @@ def main():
         "unit": "GB/s",
         "frac": achieved / PEAK_HBM,
         "traffic": None,
+        "traffic_source": None,
         "avg_launch_ms": avg_s * 1e3,
         "launches_per_step": dom_launches / args.steps,
         "alg_bytes_per_record": ALG_BYTES.get(dom_name, 0),
@@ -176,6 +184,9 @@ def main():
         "pipeline_alg_bytes_per_record": pipeline_bytes(args, dims),
         "pipeline_frac": value / world * pipeline_bytes(args, dims) / PEAK_HBM,
     }
+    traffic = pmc_traffic(args, dom_name)
+    if traffic is not None:
+        roofline["traffic"], roofline["traffic_source"] = traffic
     kernel_ms_per_step = {k: round(v[0] / args.steps, 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}
 
     cpu = None
@@ -213,6 +224,22 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(args, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
+    (tools/pmc_passes.sh -> tools/pmc_traffic.py), if it was measured on this engine source and
+    this workload; else None (the roofline then reports traffic null)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import source_hash
+
+    path = args.traffic_json
+    if not path or not os.path.exists(path) or args.records != 100_000_000 or args.cells != 10_000:
+        return None
+    d = json.load(open(path))
+    if d.get("source_sha256") != source_hash(ROOT) or kernel not in d.get("kernels", {}):
+        return None
+    return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
 
 
 def cpu_baseline(data, args):
