@@ -214,6 +214,34 @@ int sct_cell_metrics_gene_partials(const sct_plan_t* plan, const sct_records_t* 
 int sct_finalize_partials(int32_t mode, const int64_t* partials, int64_t rows, int64_t* out_ints,
                           double* out_floats, void* stream);
 
+/* ---- tag sort (TagSortBam / bam.sort_by_tags_and_queryname, bam.py:638-709;
+ *      platform.py:55-104) ---- */
+#define SCT_ORDER_CELL 0          /* CB only: what cell metrics need (input order kept within a cell) */
+#define SCT_ORDER_CELL_UMI_GENE 1 /* CB, UB, GE: TagSortBam's order for GatherCellMetrics          */
+#define SCT_ORDER_GENE_CELL_UMI 2 /* GE, CB, UB: TagSortBam's order for GatherGeneMetrics          */
+
+/* Device workspace bytes for sct_tag_sort / sct_verify_sort of plan->n_records
+ * records (plan: n_records and the three dictionary sizes; mode, float_mode
+ * and flags are ignored). */
+int sct_tag_sort_workspace_size(const sct_plan_t* plan, size_t* bytes);
+
+/* Stable sort of `in` into `out` (caller-allocated device columns of n records,
+ * written; must not alias `in`) by the `order` fields (dictionary ids: ranks of
+ * the sorted tag strings, a missing tag first, as bam.get_tag_or_default(..., "")
+ * sorts), then by `tiebreak` (nullable device int32 ids in [0, n_tiebreak_ids):
+ * the query-name rank).  Without a tiebreak, ties keep input order (Python's
+ * sorted() is stable).  Does not synchronize. */
+int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t* tiebreak,
+                 int32_t n_tiebreak_ids, int32_t order, const sct_records_t* out, void* workspace,
+                 size_t workspace_bytes, void* stream);
+
+/* verify_sort (bam.py:712-724; VerifyBamSort, platform.py:107-143): *first_violation
+ * (host) = the first index j with record j ordered before record j-1, or -1 if
+ * `rec` is sorted by `order` (then `tiebreak`, if given).  Synchronizes `stream`. */
+int sct_verify_sort(const sct_plan_t* plan, const sct_records_t* rec, const int32_t* tiebreak,
+                    int32_t order, void* workspace, size_t workspace_bytes,
+                    int64_t* first_violation /* host */, void* stream);
+
 /* Optional kernel timing: while enabled, every kernel launch is bracketed by
  * HIP events on its launch stream.  sct_profile_read waits for the events,
  * fills up to `max_kernels` (name, total ms, launches) triples (host arrays;

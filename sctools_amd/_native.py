@@ -34,7 +34,9 @@ RECORD_COLUMNS = ("cell", "umi", "gene", "ref", "pos", "gq_sum", "gq_len", "gq_g
 
 EXPORTED = ("sct_abi_version", "sct_last_error", "sct_workspace_size", "sct_count_entities",
             "sct_compute_metrics", "sct_gene_partials", "sct_cell_metrics_gene_partials",
-            "sct_finalize_partials", "sct_profile_enable", "sct_profile_read")
+            "sct_finalize_partials", "sct_profile_enable", "sct_profile_read", "sct_tag_sort_workspace_size",
+            "sct_tag_sort", "sct_verify_sort")
+ORDER_CELL, ORDER_CELL_UMI_GENE, ORDER_GENE_CELL_UMI = 0, 1, 2
 PLAN_GENE_PARTIALS = 0x1
 
 
@@ -93,6 +95,14 @@ def load() -> ctypes.CDLL:
                                                  ctypes.c_size_t, vp, vp, i64, ctypes.POINTER(i64), vp, vp]
     L.sct_finalize_partials.restype = ctypes.c_int
     L.sct_finalize_partials.argtypes = [i32, vp, i64, vp, vp, vp]
+    L.sct_tag_sort_workspace_size.restype = ctypes.c_int
+    L.sct_tag_sort_workspace_size.argtypes = [ctypes.POINTER(Plan), ctypes.POINTER(ctypes.c_size_t)]
+    L.sct_tag_sort.restype = ctypes.c_int
+    L.sct_tag_sort.argtypes = [ctypes.POINTER(Plan), ctypes.POINTER(Records), vp, i32, i32, ctypes.POINTER(Records),
+                               vp, ctypes.c_size_t, vp]
+    L.sct_verify_sort.restype = ctypes.c_int
+    L.sct_verify_sort.argtypes = [ctypes.POINTER(Plan), ctypes.POINTER(Records), vp, i32, vp, ctypes.c_size_t,
+                                  ctypes.POINTER(ctypes.c_int64), vp]
     L.sct_profile_enable.restype = ctypes.c_int
     L.sct_profile_enable.argtypes = [ctypes.c_int]
     L.sct_profile_read.restype = ctypes.c_int

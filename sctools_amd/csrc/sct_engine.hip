@@ -31,6 +31,7 @@
 #include "radix.h"
 #include "reduce.h"
 #include "segment.h"
+#include "tagsort.h"
 #include "util.h"
 
 using namespace sct;
@@ -440,6 +441,67 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   return SCT_OK;
 }
 
+// ---- tag sort ----
+struct SortLayout {
+  size_t recs, ka, kb, va, vb, counts, offsets, sums, bad, total;
+};
+
+SortLayout sort_layout(int64_t n) {
+  SortLayout L;
+  const int64_t n1 = n > 0 ? n : 1;
+  const int64_t tiles = cdiv(n1, kTile);
+  const int64_t m = (int64_t)kRadix * tiles;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += align_up(bytes);
+    return o;
+  };
+  L.recs = take(sizeof(PackedRec) * (size_t)n1);
+  L.ka = take(sizeof(uint64_t) * (size_t)n1);
+  L.kb = take(sizeof(uint64_t) * (size_t)n1);
+  L.va = take(sizeof(uint32_t) * (size_t)n1);
+  L.vb = take(sizeof(uint32_t) * (size_t)n1);
+  L.counts = take(sizeof(uint32_t) * (size_t)m);
+  L.offsets = take(sizeof(uint32_t) * (size_t)m);
+  L.sums = take(sizeof(uint64_t) * (size_t)(cdiv(m, kScanChunk) + 1));
+  L.bad = take(sizeof(uint64_t));
+  L.total = off;
+  return L;
+}
+
+// the order's fields, most significant first (+ the tiebreak, least significant)
+int order_fields(int32_t order, const sct_plan_t* plan, bool tie, int32_t n_tie, KeyField* f, int* nf) {
+  const KeyField cell{0, bitlen((uint64_t)plan->n_cell_ids)}, umi{1, bitlen((uint64_t)plan->n_umi_ids)},
+      gene{2, bitlen((uint64_t)plan->n_gene_ids)};
+  int k = 0;
+  if (order == SCT_ORDER_CELL) {
+    f[k++] = cell;
+  } else if (order == SCT_ORDER_CELL_UMI_GENE) {
+    f[k++] = cell, f[k++] = umi, f[k++] = gene;
+  } else if (order == SCT_ORDER_GENE_CELL_UMI) {
+    f[k++] = gene, f[k++] = cell, f[k++] = umi;
+  } else {
+    return fail(SCT_EINVAL, "unknown sort order %d", order);
+  }
+  if (tie) {
+    if (n_tie <= 0) return fail(SCT_EINVAL, "n_tiebreak_ids must be positive");
+    f[k++] = KeyField{3, bitlen((uint64_t)n_tie)};
+  }
+  *nf = k;
+  return SCT_OK;
+}
+
+int check_sort_args(const sct_plan_t* plan, const sct_records_t* rec) {
+  if (!plan || !rec) return fail(SCT_EINVAL, "NULL plan or records");
+  if (plan->n_records < 0 || plan->n_records > (int64_t)0x7FFFFFFF)
+    return fail(SCT_EINVAL, "n_records %lld out of range [0, 2^31)", (long long)plan->n_records);
+  if (rec->n != plan->n_records) return fail(SCT_EINVAL, "records.n != plan.n_records");
+  if (plan->n_cell_ids <= 0 || plan->n_gene_ids <= 0 || plan->n_umi_ids <= 0)
+    return fail(SCT_EINVAL, "dictionary sizes must be positive");
+  return SCT_OK;
+}
+
 }  // namespace
 
 // ======================================================================================
@@ -568,6 +630,84 @@ int sct_cell_metrics_gene_partials(const sct_plan_t* plan, const sct_records_t* 
   }
   return pipeline(plan, rec, gene_is_mito, workspace, workspace_bytes, out_ints, out_floats, capacity, n_rows,
                   gene_partials, s);
+}
+
+int sct_tag_sort_workspace_size(const sct_plan_t* plan, size_t* bytes) {
+  if (!plan || !bytes) return fail(SCT_EINVAL, "NULL argument");
+  *bytes = sort_layout(plan->n_records).total;
+  return SCT_OK;
+}
+
+int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t* tiebreak, int32_t n_tiebreak_ids,
+                 int32_t order, const sct_records_t* out, void* workspace, size_t workspace_bytes, void* stream) {
+  last_error().clear();
+  int rc = check_sort_args(plan, in);
+  if (rc) return rc;
+  if (!out || out->n != in->n) return fail(SCT_EINVAL, "out must hold records.n records");
+  KeyField f[4];
+  int nf = 0;
+  rc = order_fields(order, plan, tiebreak != nullptr, n_tiebreak_ids, f, &nf);
+  if (rc) return rc;
+  const int64_t n = in->n;
+  if (n == 0) return SCT_OK;
+  const SortLayout L = sort_layout(n);
+  if (!workspace || workspace_bytes < L.total)
+    return fail(SCT_ENOMEM, "workspace too small (%zu < %zu)", workspace_bytes, L.total);
+  hipStream_t s = (hipStream_t)stream;
+  uint4* recs = at<uint4>(workspace, L.recs);
+  SortBuffers B{at<uint64_t>(workspace, L.ka), at<uint64_t>(workspace, L.kb), at<uint32_t>(workspace, L.va),
+                at<uint32_t>(workspace, L.vb), at<uint32_t>(workspace, L.counts), at<uint32_t>(workspace, L.offsets),
+                at<uint64_t>(workspace, L.sums)};
+  const dim3 grid((unsigned)cdiv(n, kBlock));
+  LAUNCH("tag_pack", k_pack, grid, dim3(kBlock), s, *in, recs);
+  // rounds: fields from the least significant end, packed greedily into <= 64-bit keys
+  const uint32_t* perm = nullptr;
+  int hi = nf;  // fields [lo, hi) of the next round (most significant first)
+  while (hi > 0) {
+    int lo = hi, bits = 0;
+    while (lo > 0 && bits + f[lo - 1].bits <= 64) bits += f[--lo].bits;
+    RoundKey rk{};
+    rk.nf = hi - lo;
+    rk.bits = bits;
+    for (int i = 0; i < rk.nf; i++) rk.f[i] = f[lo + i];
+    LAUNCH("tag_keys", k_round_keys, grid, dim3(kBlock), s, (const uint4*)recs, tiebreak, perm, n, rk, B.ka, B.va);
+    int which = 0;
+    rc = radix_sort(B, n, bits, &which, s);
+    if (rc) return rc;
+    perm = which ? B.vb : B.va;
+    hi = lo;
+  }
+  LAUNCH("tag_unpack", k_unpack, grid, dim3(kBlock), s, (const uint4*)recs, perm, n, *out);
+  return SCT_OK;
+}
+
+int sct_verify_sort(const sct_plan_t* plan, const sct_records_t* rec, const int32_t* tiebreak, int32_t order,
+                    void* workspace, size_t workspace_bytes, int64_t* first_violation, void* stream) {
+  last_error().clear();
+  int rc = check_sort_args(plan, rec);
+  if (rc) return rc;
+  if (!first_violation) return fail(SCT_EINVAL, "first_violation is NULL");
+  KeyField f[4];
+  int nf = 0;
+  rc = order_fields(order, plan, false, 0, f, &nf);
+  if (rc) return rc;
+  *first_violation = -1;
+  if (rec->n < 2) return SCT_OK;
+  const SortLayout L = sort_layout(rec->n);
+  if (!workspace || workspace_bytes < L.total)
+    return fail(SCT_ENOMEM, "workspace too small (%zu < %zu)", workspace_bytes, L.total);
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long* bad = at<unsigned long long>(workspace, L.bad);
+  const unsigned long long none = (unsigned long long)rec->n;
+  HIPCHK(hipMemsetAsync(bad, 0xFF, sizeof(unsigned long long), s));  // no violation: ~0
+  for (int i = nf; i < 3; i++) f[i] = KeyField{0, 0};
+  LAUNCH("tag_verify", k_verify_order, dim3((unsigned)cdiv(rec->n - 1, kBlock)), dim3(kBlock), s, *rec, tiebreak,
+         f[0], f[1], f[2], nf, bad);
+  unsigned long long h = 0;
+  HIPCHK(hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *first_violation = h >= none ? -1 : (int64_t)h;
+  return SCT_OK;
 }
 
 int sct_finalize_partials(int32_t mode, const int64_t* partials, int64_t rows, int64_t* out_ints, double* out_floats,

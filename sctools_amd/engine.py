@@ -183,6 +183,43 @@ class Engine:
                                                self._stream()))
         return ints[:rows], floats[:rows]
 
+    # ---- tag sort (TagSortBam / bam.sort_by_tags_and_queryname, bam.py:638-709) ----
+    def _sort_ws(self, plan: N.Plan) -> torch.Tensor:
+        nbytes = ctypes.c_size_t(0)
+        N.check(self.lib.sct_tag_sort_workspace_size(ctypes.byref(plan), ctypes.byref(nbytes)))
+        need = int(nbytes.value)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = None
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def tag_sort(self, cols, dims: Dims, order: str = "cell_umi_gene", tiebreak: Optional[torch.Tensor] = None,
+                 n_tiebreak_ids: int = 0) -> Dict[str, torch.Tensor]:
+        """Stably sorted copy of the columns by `order` ('cell', 'cell_umi_gene', 'gene_cell_umi'), then by
+        `tiebreak` ids (the query-name rank) if given; ties keep input order, as sorted() does."""
+        rec = records_struct(cols)
+        out = {c: torch.empty_like(cols[c]) for c in N.RECORD_COLUMNS}
+        orec = records_struct(out)
+        plan = self._plan(rec.n, "cell", "exact", dims)
+        ws = self._sort_ws(plan)
+        tb = ctypes.c_void_p(tiebreak.data_ptr()) if tiebreak is not None else None
+        N.check(self.lib.sct_tag_sort(ctypes.byref(plan), ctypes.byref(rec), tb, int(n_tiebreak_ids), ORDERS[order],
+                                      ctypes.byref(orec), ctypes.c_void_p(ws.data_ptr()), ws.numel(), self._stream()))
+        return out
+
+    def verify_sort(self, cols, dims: Dims, order: str = "cell_umi_gene",
+                    tiebreak: Optional[torch.Tensor] = None) -> int:
+        """verify_sort (bam.py:712-724): -1 if sorted, else the first out-of-order record index."""
+        rec = records_struct(cols)
+        plan = self._plan(rec.n, "cell", "exact", dims)
+        ws = self._sort_ws(plan)
+        tb = ctypes.c_void_p(tiebreak.data_ptr()) if tiebreak is not None else None
+        out = ctypes.c_int64(0)
+        N.check(self.lib.sct_verify_sort(ctypes.byref(plan), ctypes.byref(rec), tb, ORDERS[order],
+                                         ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.byref(out),
+                                         self._stream()))
+        return int(out.value)
+
     # ---- profiling (HIP events inside the library) ----
     def profile_enable(self, on: bool = True):
         self.lib.sct_profile_enable(1 if on else 0)
@@ -195,6 +232,8 @@ class Engine:
         k = self.lib.sct_profile_read(names, ms, launches, cap)
         return {names[i].decode(): (float(ms[i]), int(launches[i])) for i in range(min(k, cap))}
 
+
+ORDERS = {"cell": N.ORDER_CELL, "cell_umi_gene": N.ORDER_CELL_UMI_GENE, "gene_cell_umi": N.ORDER_GENE_CELL_UMI}
 
 _engines: Dict[str, Engine] = {}
 

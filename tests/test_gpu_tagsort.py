@@ -1,0 +1,186 @@
+"""On-GPU tag sort (sct_tag_sort / sct_verify_sort) against the reference's sort semantics.
+
+The reference sorts with Python's stable sorted() by tag values then query name
+(bam.sort_by_tags_and_queryname, bam.py:638-709) and checks with verify_sort
+(bam.py:712-724).  Pinned by the reference's own fixtures: its
+`cell-gene-umi-queryname-sorted.bam` is exactly `unsorted.bam` in (CB, UB, GE,
+query name) order (checked by test_fixture_order_is_lexsort on CPU), so tag-sorting
+`unsorted.bam` on the GPU must reproduce that file's records and, through the
+Welford pipeline, the reference's metric CSVs byte for byte.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import helpers as H
+from sctools_amd import _native as N
+from sctools_amd import bam as B
+
+ORDERS = {"cell": ("cell",), "cell_umi_gene": ("cell", "umi", "gene"), "gene_cell_umi": ("gene", "cell", "umi")}
+
+
+def qname_ranks(name):
+    q = [r.query_name for r in B.open_alignments(os.path.join(H.GOLDEN, "bam", name + ".bam"), "rb")]
+    rank = {v: i for i, v in enumerate(sorted(set(q)))}
+    return np.array([rank[v] for v in q], dtype=np.int32), len(rank)
+
+
+def np_order(arrays, order, tie=None):
+    keys = [arrays[f] for f in reversed(ORDERS[order])]
+    if tie is not None:
+        keys = [tie] + keys
+    return np.lexsort(keys)  # stable: ties keep input order, as sorted() does
+
+
+def test_fixture_order_is_lexsort():
+    """CPU: the reference's sorted fixture is lexsort(CB, UB, GE, query name) of unsorted.bam."""
+    u = H.bam_columns("unsorted", "cell")
+    s = H.bam_columns("cell-gene-umi-queryname-sorted", "cell")
+    tie, _ = qname_ranks("unsorted")
+    order = np_order(u.arrays, "cell_umi_gene", tie)
+    for c in N.RECORD_COLUMNS:
+        assert np.array_equal(u.arrays[c][order], s.arrays[c]), c
+
+
+def test_invalid_order_is_rejected_without_a_gpu():
+    import ctypes
+
+    lib = N.load()
+    plan = N.Plan(n_records=0, n_cell_ids=1, n_gene_ids=1, n_umi_ids=1)
+    rec = N.Records(n=0)
+    rc = lib.sct_tag_sort(ctypes.byref(plan), ctypes.byref(rec), None, 0, 9, ctypes.byref(rec), None, 0, None)
+    assert rc == -1 and b"order" in lib.sct_last_error()
+    nbytes = ctypes.c_size_t(0)
+    plan.n_records = 1000
+    assert lib.sct_tag_sort_workspace_size(ctypes.byref(plan), ctypes.byref(nbytes)) == 0
+    assert nbytes.value >= 56 * 1000  # packed record + two key/value buffer pairs
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from sctools_amd import engine as E
+
+    return E.get_engine("cuda:0")
+
+
+def to_dev(eng, arrays):
+    from sctools_amd import engine as E
+
+    return E.to_device(arrays, eng.device)
+
+
+def to_host(cols):
+    out = {c: t.cpu().numpy() for c, t in cols.items()}
+    for c in ("gq_sum", "gq_len", "gq_gt30"):
+        out[c] = out[c].view(np.uint16)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["cell", "gene"])
+def test_unsorted_bam_tag_sorted_on_gpu_matches_reference(eng, mode):
+    from sctools_amd import engine as E
+
+    u = H.bam_columns("unsorted", mode)
+    tie, n_tie = qname_ranks("unsorted")
+    d = E.Dims(len(u.cells), len(u.genes), len(u.umis))
+    cols = eng.tag_sort(to_dev(eng, u.arrays), d, "cell_umi_gene", torch.from_numpy(tie).to(eng.device), n_tie)
+    host = to_host(cols)
+    ref = H.bam_columns("cell-gene-umi-queryname-sorted", mode)
+    for c in N.RECORD_COLUMNS:
+        assert np.array_equal(host[c], ref.arrays[c]), c
+    assert eng.verify_sort(cols, d, "cell_umi_gene", torch.from_numpy(tie[np_order(u.arrays, "cell_umi_gene", tie)])
+                           .to(eng.device)) == -1
+    # and the metrics of the sorted records are the reference's, byte for byte (Welford)
+    mito, _ = u.gene_flags()
+    gm = torch.from_numpy(np.ascontiguousarray(mito, dtype=np.uint8)).to(eng.device)
+    gi, gf = eng.compute(cols, mode, d, gm, gm, float_mode="welford")
+    got = H.render(mode, gi.cpu().numpy(), gf.cpu().numpy(), host, u.cells.names, u.genes.names)
+    assert got == H.golden_text("cell-gene-umi-queryname-sorted", mode)
+
+
+def shuffled_synth(n, seed, n_cells=300):
+    from sctools_amd import synth
+
+    d = synth.generate(synth.SynthConfig(n_reads=n, n_cells=n_cells, n_genes=2000, seed=seed), device="cpu")
+    arrays = to_host(d.cols)
+    perm = np.random.default_rng(seed).permutation(n)
+    return d, arrays, {c: np.ascontiguousarray(a[perm]) for c, a in arrays.items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", list(ORDERS))
+@pytest.mark.parametrize("with_tie", [False, True])
+def test_tag_sort_matches_numpy_lexsort(eng, order, with_tie):
+    from sctools_amd import engine as E
+
+    d, _, arrays = shuffled_synth(200_000, 5)
+    n = arrays["cell"].shape[0]
+    tie = np.random.default_rng(1).integers(0, 1000, n).astype(np.int32) if with_tie else None
+    dims = E.Dims(d.n_cell_ids, d.n_gene_ids, d.n_umi_ids)
+    out = eng.tag_sort(to_dev(eng, arrays), dims, order, None if tie is None else torch.from_numpy(tie).to(eng.device),
+                       1000)
+    host = to_host(out)
+    idx = np_order(arrays, order, tie)
+    for c in N.RECORD_COLUMNS:
+        assert np.array_equal(host[c], arrays[c][idx]), c
+
+
+@pytest.mark.gpu
+def test_tag_sort_with_keys_wider_than_64_bits(eng):
+    """Inflated dictionary sizes: the fields need two 64-bit rounds ([gene | tie], then [cell | umi])."""
+    from sctools_amd import engine as E
+
+    d, _, arrays = shuffled_synth(100_000, 6)
+    n = arrays["cell"].shape[0]
+    tie = np.random.default_rng(2).integers(0, 1 << 20, n).astype(np.int32)
+    dims = E.Dims(1 << 28, 1 << 30, 1 << 30)
+    out = eng.tag_sort(to_dev(eng, arrays), dims, "cell_umi_gene", torch.from_numpy(tie).to(eng.device), 1 << 20)
+    host = to_host(out)
+    idx = np_order(arrays, "cell_umi_gene", tie)
+    for c in N.RECORD_COLUMNS:
+        assert np.array_equal(host[c], arrays[c][idx]), c
+
+
+@pytest.mark.gpu
+def test_verify_sort_finds_the_first_violation(eng):
+    from sctools_amd import engine as E
+
+    d, sorted_arrays, arrays = shuffled_synth(50_000, 7)
+    dims = E.Dims(d.n_cell_ids, d.n_gene_ids, d.n_umi_ids)
+    assert eng.verify_sort(to_dev(eng, sorted_arrays), dims, "cell") == -1
+    c = arrays["cell"]
+    first = int(np.argmax(c[1:] < c[:-1])) + 1
+    assert eng.verify_sort(to_dev(eng, arrays), dims, "cell") == first
+    key = np.lexsort((arrays["gene"], arrays["umi"], arrays["cell"]))
+    s = {k: v[key] for k, v in arrays.items()}
+    assert eng.verify_sort(to_dev(eng, s), dims, "cell_umi_gene") == -1
+    assert eng.verify_sort(to_dev(eng, s), dims, "gene_cell_umi") > 0
+
+
+@pytest.mark.gpu
+def test_unsorted_input_cell_metrics_after_gpu_sort(eng):
+    """Config 5 shape: globally shuffled records, GPU sort by cell, then the exact-sum cell and
+    grouped gene metrics equal those of the cell-sorted original (integers and floats exactly)."""
+    from sctools_amd import engine as E
+    from sctools_amd import synth
+
+    data = synth.generate(synth.SynthConfig(n_reads=4_000_000, n_cells=400, n_genes=5000, seed=9), device=eng.device)
+    dims = E.Dims(data.n_cell_ids, data.n_gene_ids, data.n_umi_ids)
+    mito = torch.from_numpy(data.gene_is_mito).to(eng.device)
+    perm = torch.randperm(data.cols["cell"].numel(), generator=torch.Generator().manual_seed(3)).to(eng.device)
+    shuffled = {c: t[perm].contiguous() for c, t in data.cols.items()}
+    assert eng.verify_sort(shuffled, dims, "cell") > 0
+    regrouped = eng.tag_sort(shuffled, dims, "cell")
+    assert eng.verify_sort(regrouped, dims, "cell") == -1
+    ci0, cf0, p0 = eng.cell_and_gene(data.cols, dims, mito)
+    ci0, cf0, p0 = ci0.cpu().numpy(), cf0.cpu().numpy(), p0.clone()
+    ci1, cf1, p1 = eng.cell_and_gene(regrouped, dims, mito)
+    ci1, cf1 = ci1.cpu().numpy(), cf1.cpu().numpy()
+    ent = N.I_ENTITY
+    keep = [i for i in range(ci0.shape[1]) if i != ent]  # first-record index differs; the rest must not
+    assert np.array_equal(ci0[:, keep], ci1[:, keep])
+    assert np.array_equal(np.nan_to_num(cf0, nan=-7.0), np.nan_to_num(cf1, nan=-7.0))
+    assert torch.equal(p0, p1)
