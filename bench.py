@@ -40,6 +40,9 @@ ALG_BYTES = {
     "big_bucket": 18,        # read payload w0 + w1 (16) of the big buckets' records, write dflags (2)
     "gene_emit": 32,         # read gene/bits/xf/dflags/uy/gq (16), write 16-byte gene payload
     "gene_reduce": 16,       # read the 16-byte gene payload
+    "tag_pack": 64,          # config 5: read the 32-byte SoA record, write it packed
+    "tag_keys": 28,          # read the packed record's key words (16), write key 8 + index 4
+    "tag_unpack": 64,        # gather the packed record (32), write the SoA columns (32)
     "radix_downsweep": 24,   # global-sort path: read key 8 + value 4, write key 8 + value 4
     "radix_upsweep": 8,
     "reduce_sorted": 12,
@@ -69,6 +72,9 @@ def parse():
     ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="target seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
+                    help="2: cell-sorted records (default); 5: globally shuffled records, 30%% NH>1, 40%% duplicates, "
+                         "sorted by cell on the GPU inside every step (SURVEY.md 8(d) config 5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"),
                     help="rocprofv3 --pmc per-kernel HBM bytes (tools/pmc_passes.sh) for roofline.traffic")
     return ap.parse_args()
@@ -99,14 +105,25 @@ def main():
     t0 = time.time()
     cfg = synth.SynthConfig(n_reads=args.records, n_cells=args.cells, n_genes=args.genes, sigma=1.0,
                             seed=args.seed + 1000 * rank)
+    if args.config == 5:
+        cfg.p_nh1, cfg.p_dup = 0.70, 0.40
     data = synth.generate(cfg, device=dev, chunk=16_000_000)
+    if args.config == 5:  # global permutation: the step must regroup records by cell itself
+        g = torch.Generator(device=dev)
+        g.manual_seed(args.seed + 1 + 1000 * rank)
+        perm = torch.randperm(args.records, generator=g, device=dev)
+        data.cols = {c: t[perm].contiguous() for c, t in data.cols.items()}
+        del perm
     torch.cuda.synchronize()
     if rank == 0:
         log("generated %d records/rank in %.1fs" % (args.records, time.time() - t0))
     dims = E.Dims(data.n_cell_ids, data.n_gene_ids, data.n_umi_ids)
     mito = torch.from_numpy(data.gene_is_mito).to(dev)
     multi = torch.from_numpy(data.gene_is_multi).to(dev)
-    n_ent = eng.count_entities(data.cols, "cell", dims)
+    if args.config == 5:
+        n_ent = eng.count_entities(eng.tag_sort(data.cols, dims, "cell"), "cell", dims)
+    else:
+        n_ent = eng.count_entities(data.cols, "cell", dims)
     partials = torch.empty((data.n_gene_ids, 64), dtype=torch.int64, device=dev)
     host_cells = torch.empty((n_ent, 24), dtype=torch.int64, pin_memory=True)
     host_cellf = torch.empty((n_ent, 12), dtype=torch.float64, pin_memory=True)
@@ -116,12 +133,13 @@ def main():
     copy_stream = torch.cuda.Stream(device=dev)
 
     def step():
+        cols = eng.tag_sort(data.cols, dims, "cell") if args.config == 5 else data.cols
         if args.float_mode == "exact":
             # one pass: cell rows + grouped gene partials share the cell-view sort
-            ci, cf, _ = eng.cell_and_gene(data.cols, dims, mito, n_entities=n_ent, partials=partials)
+            ci, cf, _ = eng.cell_and_gene(cols, dims, mito, n_entities=n_ent, partials=partials)
         else:
-            ci, cf = eng.compute(data.cols, "cell", dims, mito, multi, float_mode=args.float_mode, n_entities=n_ent)
-            eng.gene_partials(data.cols, dims, out=partials)
+            ci, cf = eng.compute(cols, "cell", dims, mito, multi, float_mode=args.float_mode, n_entities=n_ent)
+            eng.gene_partials(cols, dims, out=partials)
         D.allreduce_partials(partials)  # RCCL over xGMI when N > 1; no-op at N = 1
         gi, gf = eng.finalize_partials(partials)
         # rows -> pinned host on a copy stream: this step's D2H overlaps the next step's kernels
@@ -208,9 +226,10 @@ def main():
             "dtype": "int64",
             "data": "synthetic (SURVEY.md 8(d) config-2 generator, generated on GPU)",
             "config": {
-                "workload": "config2: %d cell-sorted records/rank, %d cells/rank, %d genes; cell metrics + "
-                            "grouped gene metrics%s" % (args.records, args.cells, args.genes,
-                                                        " + RCCL all-reduce" if world > 1 else ""),
+                "workload": ("config2: %d cell-sorted records/rank" if args.config == 2 else
+                             "config5: %d globally shuffled records/rank (30%% NH>1, 40%% dup), GPU sort by cell + ")
+                            % args.records + ", %d cells/rank, %d genes; cell metrics + grouped gene metrics%s"
+                            % (args.cells, args.genes, " + RCCL all-reduce" if world > 1 else ""),
                 "records_per_rank": args.records,
                 "cells_per_rank": args.cells,
                 "genes": args.genes,
@@ -252,6 +271,11 @@ def cpu_baseline(data, args):
 
     def sample(n):
         n = min(n, cell.numel())
+        if args.config == 5:  # shuffled shard: any leading slice is a fair sample (sorted inside run())
+            h = {c: t[:n].cpu().numpy() for c, t in cols.items()}
+            for c in ("gq_sum", "gq_len", "gq_gt30"):
+                h[c] = h[c].view(np.uint16)
+            return n, h
         # cut at a cell boundary so every cell in the sample is complete
         c_last = int(cell[n - 1].item())
         n = int(torch.searchsorted(cell, torch.tensor([c_last], dtype=cell.dtype, device=cell.device),
@@ -263,6 +287,9 @@ def cpu_baseline(data, args):
 
     def run(h):
         t0 = time.perf_counter()
+        if args.config == 5:  # regroup by cell first, as the GPU step does (numpy stable sort)
+            order = np.argsort(h["cell"], kind="stable")
+            h = {c: a[order] for c, a in h.items()}
         O.run(h, "cell", data.gene_is_mito, data.n_gene_ids, threads=threads)
         O.run(h, "gene_grouped", data.gene_is_mito, data.n_gene_ids, threads=threads)
         return time.perf_counter() - t0
@@ -277,8 +304,10 @@ def cpu_baseline(data, args):
         "unit": "records/s",
         "cores": threads,
         "kind": "port",
-        "sample": "first %d records (%d whole cells) of rank 0's shard: oracle cell metrics + grouped gene "
-                  "metrics, %.1fs" % (n1, int(h1["cell"][-1]) + 1, t1),
+        "sample": ("first %d records (%d whole cells) of rank 0's shard: oracle cell metrics + grouped gene "
+                   "metrics, %.1fs" % (n1, int(h1["cell"][-1]) + 1, t1)) if args.config == 2 else
+                  ("first %d records of rank 0's shuffled shard: numpy stable sort by cell + oracle cell metrics + "
+                   "grouped gene metrics, %.1fs" % (n1, t1)),
     }
 
 
