@@ -1,0 +1,72 @@
+/* sct_bam.h -- native BAM -> columnar decoder for the metric path (host C++, zlib, OpenMP).
+ *
+ * Replaces the per-record pysam reads of the reference's aggregation loop
+ * (MetricAggregator.parse_molecule, aggregator.py:251-334; CellMetrics.parse_extra_fields,
+ * aggregator.py:507-530; pysam 0.16 AlignedSegment.query_alignment_qualities /
+ * get_cigar_stats) with one parallel pass: BGZF blocks are inflated concurrently,
+ * records are parsed concurrently, and the CB / UB / GE tag strings are dictionary-encoded
+ * to ids that are ranks of the sorted strings with a missing tag first (ids compare as the
+ * strings compare).  Output: the 32-byte-per-record SoA columns of include/sctools_gpu.h.
+ *
+ * The decode validates exactly as sctools_amd.columnar.columnarize (and so the reference):
+ * the FIRST offending record in file order decides the error, reported as a code below
+ * and a message (the Python layer raises the reference's exception types).
+ */
+#ifndef SCT_BAM_H
+#define SCT_BAM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCT_BAM_OK 0
+#define SCT_BAM_EIO -1          /* cannot open / read / inflate the file            */
+#define SCT_BAM_EFORMAT -2      /* not a BAM file or a truncated record             */
+#define SCT_BAM_KEYERROR -10    /* a required tag is missing (KeyError)             */
+#define SCT_BAM_TYPEERROR -11   /* missing base qualities (TypeError)               */
+#define SCT_BAM_ZERODIV -12     /* empty quality string (ZeroDivisionError)         */
+#define SCT_BAM_VALUEERROR -13  /* invalid clipping, or a record beyond the 32-byte columnar limits */
+#define SCT_BAM_EMPTY -14       /* no records (RuntimeError: StopIteration in iter_tag_groups) */
+
+#define SCT_BAM_CELL_METRICS 0 /* require CY (and CR where CB is present), as CellMetrics does   */
+#define SCT_BAM_GENE_METRICS 1 /* records of multi-gene GE values are not validated (gatherer.py:210-212) */
+
+#define SCT_BAM_TAG_CB 0
+#define SCT_BAM_TAG_UB 1
+#define SCT_BAM_TAG_GE 2
+
+typedef struct sct_bam sct_bam_t;
+
+/* Decode `path` (BAM).  n_threads <= 0: all cores.  On success *out owns the columns and
+ * dictionaries until sct_bam_close.  On a validation error *out is NULL, *bad_record (if
+ * set) is the offending record's index, and sct_bam_last_error() holds the message. */
+int sct_bam_decode(const char* path, int32_t metric_mode, int32_t n_threads, sct_bam_t** out,
+                   int64_t* bad_record);
+
+/* Message of the calling thread's last error ("" if none). */
+const char* sct_bam_last_error(void);
+
+/* Number of records. */
+int64_t sct_bam_n(const sct_bam_t* b);
+
+/* Host pointer to a column by name (the sct_records_t field names: "cell", "umi", "gene",
+ * "ref", "pos", "gq_sum", "gq_len", "gq_gt30", "bits", "xf", "cy_gt30", "cy_len",
+ * "uy_gt30", "uy_len"); NULL for an unknown name.  Valid until sct_bam_close. */
+const void* sct_bam_column(const sct_bam_t* b, const char* name);
+
+/* Dictionary of tag `which` (SCT_BAM_TAG_*): *n entries in id order; entry i is the UTF-8
+ * string bytes[offsets[i] .. offsets[i + 1]); *has_none = 1 when id 0 is the missing value
+ * (its bytes are empty). */
+int sct_bam_dictionary(const sct_bam_t* b, int32_t which, int64_t* n, const char** bytes,
+                       const int64_t** offsets, int32_t* has_none);
+
+void sct_bam_close(sct_bam_t* b);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SCT_BAM_H */

@@ -1,0 +1,97 @@
+"""
+ctypes binding of ``libsct_bam.so`` (``include/sct_bam.h``): the native BAM -> columns decoder.
+
+It replaces the per-record pysam reads of the reference's aggregation loop
+(``aggregator.py:251-334, 507-530``) for ``GatherCellMetrics`` /
+``GatherGeneMetrics`` on BAM input: BGZF blocks inflate and records parse on all
+cores, and CB / UB / GE are dictionary-encoded natively.  Validation and the
+exception classes are those of :func:`sctools_amd.columnar.columnarize` (the
+first offending record in file order decides), which the tests check against
+the pure-Python decoder on every fixture.
+"""
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsct_bam.so")
+
+OK, EIO, EFORMAT = 0, -1, -2
+KEYERROR, TYPEERROR, ZERODIV, VALUEERROR, EMPTY = -10, -11, -12, -13, -14
+CELL_METRICS, GENE_METRICS = 0, 1
+EXPORTED = ("sct_bam_decode", "sct_bam_last_error", "sct_bam_n", "sct_bam_column", "sct_bam_dictionary",
+            "sct_bam_close")
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("%s is missing: run __graft_entry__.build() (or make)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    L.sct_bam_decode.restype = ctypes.c_int
+    L.sct_bam_decode.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(vp),
+                                 ctypes.POINTER(ctypes.c_int64)]
+    L.sct_bam_last_error.restype = ctypes.c_char_p
+    L.sct_bam_last_error.argtypes = []
+    L.sct_bam_n.restype = ctypes.c_int64
+    L.sct_bam_n.argtypes = [vp]
+    L.sct_bam_column.restype = vp
+    L.sct_bam_column.argtypes = [vp, ctypes.c_char_p]
+    L.sct_bam_dictionary.restype = ctypes.c_int
+    L.sct_bam_dictionary.argtypes = [vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(vp),
+                                     ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int32)]
+    L.sct_bam_close.restype = None
+    L.sct_bam_close.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def available() -> bool:
+    return os.path.exists(LIB_PATH)
+
+
+_EXC = {KEYERROR: KeyError, TYPEERROR: TypeError, ZERODIV: ZeroDivisionError, VALUEERROR: ValueError,
+        EMPTY: RuntimeError, EFORMAT: ValueError, EIO: OSError}
+
+
+def decode(path: str, metric_mode: str = "cell", threads: int = 0):
+    """(arrays, [cell names, umi names, gene names]) -- names in id order, None first if present."""
+    from sctools_amd.columnar import COLUMNS
+
+    L = load()
+    h = ctypes.c_void_p()
+    bad = ctypes.c_int64(-1)
+    rc = L.sct_bam_decode(os.fsencode(path), CELL_METRICS if metric_mode == "cell" else GENE_METRICS,
+                          int(threads), ctypes.byref(h), ctypes.byref(bad))
+    if rc != OK:
+        msg = L.sct_bam_last_error().decode("utf-8", "replace")
+        raise _EXC.get(rc, RuntimeError)(msg)
+    try:
+        n = int(L.sct_bam_n(h))
+        arrays = {}
+        for name, dt in COLUMNS:
+            ptr = L.sct_bam_column(h, name.encode())
+            buf = (ctypes.c_char * (n * np.dtype(dt).itemsize)).from_address(ptr) if n else b""
+            arrays[name] = np.frombuffer(buf, dtype=dt, count=n).copy()
+        names = []
+        for which in range(3):
+            cnt, by, off, hn = ctypes.c_int64(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int32()
+            L.sct_bam_dictionary(h, which, ctypes.byref(cnt), ctypes.byref(by), ctypes.byref(off), ctypes.byref(hn))
+            k = int(cnt.value)
+            offs = np.frombuffer((ctypes.c_int64 * (k + 1)).from_address(off.value), dtype=np.int64).copy()
+            total = int(offs[-1])
+            raw = ctypes.string_at(by.value, total) if total else b""
+            lst = [raw[offs[i]:offs[i + 1]].decode("utf-8") for i in range(k)]
+            if hn.value:
+                lst[0] = None
+            names.append(lst)
+        return arrays, names
+    finally:
+        L.sct_bam_close(h)

@@ -1,0 +1,789 @@
+// bamdec.cpp -- native BAM -> 32-byte SoA columns (include/sct_bam.h).
+//
+// Host code: zlib for the BGZF members, OpenMP for parallel inflate / parse / intern.
+//   1. The file is memory-mapped; BGZF block boundaries are found by hopping the BSIZE
+//      fields (SAM/BAM spec 4.1).
+//   2. Windows of ~256 MB of uncompressed data: blocks inflated concurrently into one buffer
+//      (a record cut by the window end is carried into the next window), record starts
+//      found by hopping block_size, records parsed concurrently.
+//   3. Per record, the fields the reference's aggregation reads (aggregator.py:251-334,
+//      507-530) with the same validation order and exception classes as
+//      sctools_amd.columnar.record_fields: CY, CR (cell metrics), UY, the aligned qualities
+//      (pysam 0.16 getQueryStart / getQueryEnd soft-clip trimming, None when absent), XF and
+//      NH on mapped reads, then the 32-byte limits.
+//   4. CB / UB / GE strings are interned in lock-striped open-addressing tables to provisional
+//      ids, then ranked: ids are positions in the sorted string list, a missing tag first --
+//      the order of Python's sorted() on the decoded strings (bytes >= 0x80 decode to U+FFFD,
+//      as the Python reader's "ascii"/"replace" does).
+#include <fcntl.h>
+#include <omp.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <chrono>
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/sct_bam.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+// bits / xf codes: sctools_amd/columnar.py, include/sctools_gpu.h
+enum : uint8_t {
+  B_UNMAPPED = 1u << 0,
+  B_REVERSE = 1u << 1,
+  B_DUPLICATE = 1u << 2,
+  B_SPLICED = 1u << 3,
+  B_NH1 = 1u << 4,
+  B_PERFECT_UMI = 1u << 5,
+  B_HAS_CB = 1u << 6,
+  B_PERFECT_CB = 1u << 7,
+};
+enum : uint8_t { XF_ABSENT = 0, XF_CODING, XF_INTRONIC, XF_UTR, XF_INTERGENIC, XF_OTHER };
+
+inline uint16_t rd16(const uint8_t* p) {
+  uint16_t v;
+  memcpy(&v, p, 2);
+  return v;
+}
+inline uint32_t rd32(const uint8_t* p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+
+// ---------------- string interning ----------------
+inline uint64_t hash_bytes(const char* p, size_t n) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a, then a mix
+  for (size_t i = 0; i < n; i++) h = (h ^ (uint8_t)p[i]) * 1099511628211ull;
+  h ^= h >> 29;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 32;
+  return h;
+}
+
+class Interner {
+ public:
+  static constexpr int kStripes = 256;
+  Interner() : next_(1) {}
+  // provisional id >= 1 of the string
+  int32_t intern(const char* p, size_t n) { return intern(p, n, hash_bytes(p, n)); }
+  int32_t intern(const char* p, size_t n, uint64_t h) {
+    Stripe& s = stripes_[h & (kStripes - 1)];
+    std::lock_guard<std::mutex> lk(s.m);
+    if (s.slots.empty()) s.slots.assign(64, Slot{0, 0, 0, 0});
+    size_t mask = s.slots.size() - 1;
+    size_t i = (h >> 8) & mask;
+    while (true) {
+      Slot& e = s.slots[i];
+      if (e.pid == 0) break;
+      if (e.hash == h && e.len == n && memcmp(s.arena.data() + e.off, p, n) == 0) return e.pid;
+      i = (i + 1) & mask;
+    }
+    const int32_t pid = next_.fetch_add(1);
+    Slot ne{h, (uint32_t)s.arena.size(), (uint32_t)n, pid};
+    s.arena.append(p, n);
+    s.slots[i] = ne;
+    if (++s.used * 2 > s.slots.size()) grow(s);
+    return pid;
+  }
+  int32_t count() const { return next_.load() - 1; }
+  // all (string, provisional id)
+  void collect(std::vector<std::pair<std::string, int32_t>>& out) const {
+    for (const Stripe& s : stripes_)
+      for (const Slot& e : s.slots)
+        if (e.pid) out.emplace_back(std::string(s.arena.data() + e.off, e.len), e.pid);
+  }
+
+ private:
+  struct Slot {
+    uint64_t hash;
+    uint32_t off, len;
+    int32_t pid;
+  };
+  struct Stripe {
+    std::mutex m;
+    std::vector<Slot> slots;
+    std::string arena;
+    size_t used = 0;
+  };
+  static void grow(Stripe& s) {
+    std::vector<Slot> old;
+    old.swap(s.slots);
+    s.slots.assign(old.size() * 2, Slot{0, 0, 0, 0});
+    const size_t mask = s.slots.size() - 1;
+    for (const Slot& e : old) {
+      if (!e.pid) continue;
+      size_t i = (e.hash >> 8) & mask;
+      while (s.slots[i].pid) i = (i + 1) & mask;
+      s.slots[i] = e;
+    }
+  }
+  Stripe stripes_[kStripes];
+  std::atomic<int32_t> next_;
+};
+
+// ---------------- BGZF ----------------
+struct Block {
+  uint64_t off;
+  uint32_t csize, isize;
+};
+
+int scan_blocks(const uint8_t* f, uint64_t size, std::vector<Block>& blocks) {
+  uint64_t off = 0;
+  while (off < size) {
+    if (size - off < 18 || f[off] != 31 || f[off + 1] != 139 || f[off + 2] != 8 || !(f[off + 3] & 4))
+      return fail(SCT_BAM_EFORMAT, "not a BGZF block at byte %llu", (unsigned long long)off);
+    const uint16_t xlen = rd16(f + off + 10);
+    uint64_t p = off + 12, end = off + 12 + xlen;
+    int64_t bsize = -1;
+    while (p + 4 <= end) {
+      const uint16_t slen = rd16(f + p + 2);
+      if (f[p] == 66 && f[p + 1] == 67 && slen == 2) bsize = rd16(f + p + 4);
+      p += 4 + slen;
+    }
+    if (bsize < 0 || off + (uint64_t)bsize + 1 > size)
+      return fail(SCT_BAM_EFORMAT, "bad BGZF block size at byte %llu", (unsigned long long)off);
+    const uint32_t csize = (uint32_t)bsize + 1;
+    const uint32_t isize = rd32(f + off + csize - 4);
+    blocks.push_back(Block{off, csize, isize});
+    off += csize;
+  }
+  return SCT_BAM_OK;
+}
+
+bool inflate_block(const uint8_t* f, const Block& b, uint8_t* out, z_stream& z) {
+  const uint16_t xlen = rd16(f + b.off + 10);
+  const uint64_t data = b.off + 12 + xlen;
+  const uint32_t clen = b.csize - 12 - xlen - 8;
+  if (inflateReset(&z) != Z_OK) return false;
+  z.next_in = const_cast<Bytef*>(f + data);
+  z.avail_in = clen;
+  z.next_out = out;
+  z.avail_out = b.isize;
+  const int rc = inflate(&z, Z_FINISH);
+  return rc == Z_STREAM_END && z.avail_out == 0;
+}
+
+// ---------------- records ----------------
+struct Columns {
+  std::vector<int32_t> cell, umi, gene, ref, pos;
+  std::vector<uint16_t> gq_sum, gq_len, gq_gt30;
+  std::vector<uint8_t> bits, xf, cy_gt30, cy_len, uy_gt30, uy_len;
+  void resize(size_t n) {
+    cell.resize(n), umi.resize(n), gene.resize(n), ref.resize(n), pos.resize(n);
+    gq_sum.resize(n), gq_len.resize(n), gq_gt30.resize(n);
+    bits.resize(n), xf.resize(n), cy_gt30.resize(n), cy_len.resize(n), uy_gt30.resize(n), uy_len.resize(n);
+  }
+};
+
+// a tag's value as the Python reader sees it: a string (Z, H, A; integers printed in decimal
+// for the string tags) or an integer
+struct TagVal {
+  bool present = false, is_str = false;
+  const char* s = nullptr;
+  size_t n = 0;
+  int64_t i = 0;
+  char num[24];
+};
+
+// Z/H/A/integer value at p (type t); returns the bytes the value occupies, or 0 for an
+// unknown type
+size_t read_tag(const uint8_t* p, const uint8_t* end, char t, TagVal* v) {
+  switch (t) {
+    case 'Z':
+    case 'H': {
+      const uint8_t* z = (const uint8_t*)memchr(p, 0, end - p);
+      if (!z) return 0;
+      if (v) v->present = true, v->is_str = true, v->s = (const char*)p, v->n = z - p;
+      return z - p + 1;
+    }
+    case 'A':
+      if (v) v->present = true, v->is_str = true, v->s = (const char*)p, v->n = 1;
+      return 1;
+    case 'c':
+      if (v) v->present = true, v->i = (int8_t)p[0];
+      return 1;
+    case 'C':
+      if (v) v->present = true, v->i = p[0];
+      return 1;
+    case 's':
+      if (v) v->present = true, v->i = (int16_t)rd16(p);
+      return 2;
+    case 'S':
+      if (v) v->present = true, v->i = rd16(p);
+      return 2;
+    case 'i':
+      if (v) v->present = true, v->i = (int32_t)rd32(p);
+      return 4;
+    case 'I':
+      if (v) v->present = true, v->i = rd32(p);
+      return 4;
+    case 'f':
+      if (v) v->present = true;
+      return 4;
+    case 'd':
+      if (v) v->present = true;
+      return 8;
+    case 'B': {
+      const char sub = (char)p[0];
+      const uint32_t cnt = rd32(p + 1);
+      const size_t w = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+      if (v) v->present = true;
+      return 5 + (size_t)cnt * w;
+    }
+    default:
+      return 0;
+  }
+}
+
+// the string form of a value (the Python tag value passed through str())
+void as_str(TagVal& v) {
+  if (!v.present || v.is_str) return;
+  snprintf(v.num, sizeof(v.num), "%lld", (long long)v.i);
+  v.s = v.num;
+  v.n = strlen(v.num);
+  v.is_str = true;
+}
+
+bool str_eq(const TagVal& a, const TagVal& b) { return a.n == b.n && memcmp(a.s, b.s, a.n) == 0; }
+
+struct RecErr {
+  int code = 0;
+  std::string msg;
+};
+
+// #chars with Phred (char - 33) > 30, and the length: _quality_string_to_numeric +
+// _quality_above_threshold (aggregator.py:191-231)
+int frac_counts(const TagVal& v, uint32_t* gt, uint32_t* len, RecErr& e) {
+  if (!v.is_str) {
+    e.code = SCT_BAM_TYPEERROR;
+    e.msg = "object of type 'int' has no len()";
+    return -1;
+  }
+  if (v.n == 0) {
+    e.code = SCT_BAM_ZERODIV;
+    e.msg = "division by zero";
+    return -1;
+  }
+  uint32_t g = 0;
+  for (size_t i = 0; i < v.n; i++) g += ((uint8_t)v.s[i] > 63) ? 1u : 0u;
+  *gt = g;
+  *len = (uint32_t)v.n;
+  return 0;
+}
+
+struct Parsed {
+  int32_t ref, pos;
+  uint32_t gq_sum, gq_len, gq_gt30, cy_gt30, cy_len, uy_gt30, uy_len;
+  uint8_t bits, xf;
+  TagVal cb, ub, ge;
+};
+
+// One record (bytes after block_size).  Mirrors sctools_amd.columnar.record_fields.
+int parse_record(const uint8_t* d, uint32_t bs, bool is_cell, Parsed& o, RecErr& e) {
+  if (bs < 32) {
+    e.code = SCT_BAM_EFORMAT;
+    e.msg = "truncated BAM record";
+    return -1;
+  }
+  const int32_t ref = (int32_t)rd32(d), pos = (int32_t)rd32(d + 4);
+  const uint32_t l_read_name = d[8];
+  const uint32_t n_cigar = rd16(d + 12), flag = rd16(d + 14);
+  const uint32_t l_seq = rd32(d + 16);
+  const uint64_t cig_off = 32 + (uint64_t)l_read_name;
+  const uint64_t qual_off = cig_off + 4ull * n_cigar + (l_seq + 1) / 2;
+  const uint64_t tag_off = qual_off + l_seq;
+  if (tag_off > bs) {
+    e.code = SCT_BAM_EFORMAT;
+    e.msg = "truncated BAM record";
+    return -1;
+  }
+  const uint8_t* cig = d + cig_off;
+  const uint8_t* qual = d + qual_off;
+  // tags of interest
+  TagVal cb, cr, cy, ub, ur, uy, ge, xf, nh;
+  const uint8_t* p = d + tag_off;
+  const uint8_t* end = d + bs;
+  while (p + 3 <= end) {
+    const char a = (char)p[0], b = (char)p[1], t = (char)p[2];
+    p += 3;
+    TagVal* v = nullptr;
+    if (a == 'C' && b == 'B') v = &cb;
+    else if (a == 'C' && b == 'R') v = &cr;
+    else if (a == 'C' && b == 'Y') v = &cy;
+    else if (a == 'U' && b == 'B') v = &ub;
+    else if (a == 'U' && b == 'R') v = &ur;
+    else if (a == 'U' && b == 'Y') v = &uy;
+    else if (a == 'G' && b == 'E') v = &ge;
+    else if (a == 'X' && b == 'F') v = &xf;
+    else if (a == 'N' && b == 'H') v = &nh;
+    const size_t used = read_tag(p, end, t, v);
+    if (!used || p + used > end) {
+      e.code = SCT_BAM_EFORMAT;
+      e.msg = std::string("unsupported or truncated BAM tag type ") + t;
+      return -1;
+    }
+    p += used;
+  }
+  // gene metrics skip validation for multi-gene runs (gatherer.py:210-212)
+  bool validate = is_cell;
+  if (!is_cell) {
+    TagVal g = ge;  // str(ge) without touching ge (its string form may point into g.num)
+    as_str(g);
+    validate = !(g.present && g.n > 0 && memchr(g.s, ',', g.n));
+  }
+  uint8_t bits = 0;
+  uint32_t cg = 0, cl = 0, ug = 0, ul = 0;
+  if (is_cell) {
+    if (!cy.present) {
+      e.code = SCT_BAM_KEYERROR;
+      e.msg = "CY";
+      return -1;
+    }
+    if (frac_counts(cy, &cg, &cl, e)) return -1;
+    if (cb.present) {
+      bits |= B_HAS_CB;
+      if (!cr.present) {
+        e.code = SCT_BAM_KEYERROR;
+        e.msg = "CR";
+        return -1;
+      }
+      // CR == CB compares the Python values: equal only for equal types and contents
+      if (cr.is_str == cb.is_str && (cr.is_str ? str_eq(cr, cb) : cr.i == cb.i)) bits |= B_PERFECT_CB;
+    }
+  } else if (cb.present) {
+    bits |= B_HAS_CB;
+  }
+  if (validate) {
+    if (!uy.present) {
+      e.code = SCT_BAM_KEYERROR;
+      e.msg = "UY";
+      return -1;
+    }
+    if (frac_counts(uy, &ug, &ul, e)) return -1;
+  } else if (uy.present && (uy.is_str ? uy.n > 0 : uy.i != 0)) {  // `if uyq:` on the default-"" value
+    if (frac_counts(uy, &ug, &ul, e)) return -1;
+  }
+  if (ur.present && ub.present && ur.is_str == ub.is_str && (ur.is_str ? str_eq(ur, ub) : ur.i == ub.i))
+    bits |= B_PERFECT_UMI;
+  // query_alignment_qualities (pysam 0.16)
+  bool aq_none = l_seq == 0 || qual[0] == 0xFF;
+  uint32_t q0 = 0, q1 = 0;
+  if (!aq_none) {
+    uint32_t start = 0;
+    for (uint32_t k = 0; k < n_cigar; k++) {
+      const uint32_t c = rd32(cig + 4 * k), op = c & 0xF, len = c >> 4;
+      if (op == 5) {  // H
+        if (start != 0 && start != l_seq) {
+          e.code = SCT_BAM_VALUEERROR;
+          e.msg = "Invalid clipping in CIGAR string";
+          return -1;
+        }
+      } else if (op == 4) {  // S
+        start += len;
+      } else {
+        break;
+      }
+    }
+    uint32_t qend = l_seq;
+    for (int k = (int)n_cigar - 1; k > 0; k--) {
+      const uint32_t c = rd32(cig + 4 * k), op = c & 0xF, len = c >> 4;
+      if (op == 5) {
+        if (qend != l_seq) {
+          e.code = SCT_BAM_VALUEERROR;
+          e.msg = "Invalid clipping in CIGAR string";
+          return -1;
+        }
+      } else if (op == 4) {
+        qend -= len;
+      } else {
+        break;
+      }
+    }
+    q0 = start;
+    q1 = qend < start ? start : qend;
+  }
+  if (aq_none && validate) {
+    e.code = SCT_BAM_TYPEERROR;
+    e.msg = "'NoneType' object is not iterable";
+    return -1;
+  }
+  if (q1 == q0 && validate) {
+    e.code = SCT_BAM_ZERODIV;
+    e.msg = "division by zero";
+    return -1;
+  }
+  uint8_t x = XF_ABSENT;
+  if (xf.present) {
+    x = XF_OTHER;
+    if (xf.is_str) {
+      const std::string s(xf.s, xf.n);
+      if (s == "CODING") x = XF_CODING;
+      else if (s == "INTRONIC") x = XF_INTRONIC;
+      else if (s == "UTR") x = XF_UTR;
+      else if (s == "INTERGENIC") x = XF_INTERGENIC;
+    }
+  }
+  if (flag & 0x4) {
+    bits |= B_UNMAPPED;
+  } else {
+    int64_t nh_v = 0;
+    bool nh_int = false;
+    if (validate) {
+      if (!xf.present) {
+        e.code = SCT_BAM_KEYERROR;
+        e.msg = "XF";
+        return -1;
+      }
+      if (!nh.present) {
+        e.code = SCT_BAM_KEYERROR;
+        e.msg = "NH";
+        return -1;
+      }
+    }
+    if (nh.present && !nh.is_str) nh_v = nh.i, nh_int = true;
+    if (nh_int && nh_v == 1) bits |= B_NH1;
+    uint64_t n_len = 0;
+    for (uint32_t k = 0; k < n_cigar; k++) {
+      const uint32_t c = rd32(cig + 4 * k);
+      if ((c & 0xF) == 3) n_len += c >> 4;
+    }
+    if (n_len) bits |= B_SPLICED;
+  }
+  if (flag & 0x10) bits |= B_REVERSE;
+  if (flag & 0x400) bits |= B_DUPLICATE;
+  uint32_t s = 0, g = 0;
+  for (uint32_t k = q0; k < q1; k++) {
+    s += qual[k];
+    g += qual[k] > 30 ? 1u : 0u;
+  }
+  if (q1 - q0 > 0xFFFF || s > 0xFFFF || cl > 0xFF || ul > 0xFF) {
+    e.code = SCT_BAM_VALUEERROR;
+    e.msg = "record exceeds the 32-byte columnar limits";
+    return -1;
+  }
+  o.ref = ref, o.pos = pos, o.gq_sum = s, o.gq_len = q1 - q0, o.gq_gt30 = g;
+  o.cy_gt30 = cg, o.cy_len = cl, o.uy_gt30 = ug, o.uy_len = ul, o.bits = bits, o.xf = x;
+  o.cb = cb, o.ub = ub, o.ge = ge;
+  return 0;
+}
+
+// Per-thread direct-mapped cache in front of the shared tables: cell-sorted input repeats
+// the CB of the previous record and hot genes repeat constantly, so most lookups never take
+// a stripe lock.
+struct TagCache {
+  static constexpr int kSlots = 1024, kMaxLen = 40;
+  struct Entry {
+    uint64_t hash = 0;
+    int32_t pid = 0;
+    uint8_t len = 0;
+    char bytes[kMaxLen];
+  };
+  Entry e[kSlots];
+};
+
+int32_t intern_bytes(Interner& in, TagCache& c, const char* p, size_t n) {
+  const uint64_t h = hash_bytes(p, n);
+  TagCache::Entry& x = c.e[h & (TagCache::kSlots - 1)];
+  if (x.pid && x.hash == h && x.len == n && memcmp(x.bytes, p, n) == 0) return x.pid;
+  const int32_t pid = in.intern(p, n, h);
+  if (n <= (size_t)TagCache::kMaxLen) {
+    x.hash = h, x.pid = pid, x.len = (uint8_t)n;
+    memcpy(x.bytes, p, n);
+  }
+  return pid;
+}
+
+// intern a tag value's string form; 0 = missing.  Bytes >= 0x80 become U+FFFD (the Python
+// reader decodes with "ascii"/"replace").
+int32_t intern_tag(Interner& in, TagCache& c, TagVal& v, std::string& tmp) {
+  if (!v.present) return 0;
+  as_str(v);
+  bool ascii = true;
+  for (size_t i = 0; i < v.n; i++)
+    if ((uint8_t)v.s[i] >= 0x80) {
+      ascii = false;
+      break;
+    }
+  if (ascii) return intern_bytes(in, c, v.s, v.n);
+  tmp.clear();
+  for (size_t i = 0; i < v.n; i++) {
+    if ((uint8_t)v.s[i] < 0x80) tmp.push_back(v.s[i]);
+    else tmp.append("\xEF\xBF\xBD");
+  }
+  return intern_bytes(in, c, tmp.data(), tmp.size());
+}
+
+}  // namespace
+
+struct sct_bam {
+  Columns c;
+  int64_t n = 0;
+  std::string dict_bytes[3];
+  std::vector<int64_t> dict_off[3];
+  int32_t has_none[3] = {0, 0, 0};
+};
+
+extern "C" {
+
+const char* sct_bam_last_error(void) { return g_err.c_str(); }
+
+int sct_bam_decode(const char* path, int32_t metric_mode, int32_t n_threads, sct_bam_t** out, int64_t* bad_record) {
+  g_err.clear();
+  if (out) *out = nullptr;
+  if (bad_record) *bad_record = -1;
+  if (!path || !out) return fail(SCT_BAM_EIO, "NULL argument");
+  const bool is_cell = metric_mode == SCT_BAM_CELL_METRICS;
+  if (n_threads <= 0) n_threads = omp_get_max_threads();
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return fail(SCT_BAM_EIO, "cannot open %s", path);
+  struct stat st;
+  if (fstat(fd, &st) != 0 || st.st_size == 0) {
+    close(fd);
+    return fail(SCT_BAM_EFORMAT, "%s is empty", path);
+  }
+  const uint64_t fsize = (uint64_t)st.st_size;
+  const uint8_t* f = (const uint8_t*)mmap(nullptr, fsize, PROT_READ, MAP_PRIVATE, fd, 0);
+  close(fd);
+  if (f == MAP_FAILED) return fail(SCT_BAM_EIO, "cannot map %s", path);
+  struct Unmap {
+    const uint8_t* f;
+    uint64_t n;
+    ~Unmap() { munmap((void*)f, n); }
+  } unmap{f, fsize};
+
+  const bool timing = getenv("SCT_BAM_TIMING") != nullptr;
+  double t_inflate = 0, t_parse = 0;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double t0 = now();
+  std::vector<Block> blocks;
+  int rc = scan_blocks(f, fsize, blocks);
+  if (rc) return rc;
+  const double t_scan = now() - t0;
+
+  sct_bam* B = new sct_bam();
+  std::unique_ptr<sct_bam> guard(B);
+  Interner dicts[3];
+  std::atomic<int32_t> has_none[3];
+  for (auto& h : has_none) h = 0;
+
+  // carry + this window's inflated bytes; grown without zero-filling (inflate writes every byte)
+  struct Buf {
+    std::unique_ptr<uint8_t[]> p;
+    size_t n = 0, cap = 0;
+    uint8_t* data() { return p.get(); }
+    size_t size() const { return n; }
+    void resize(size_t m) {
+      if (m > cap) {
+        const size_t c = m + m / 4;
+        std::unique_ptr<uint8_t[]> q(new uint8_t[c]);
+        if (n) memcpy(q.get(), p.get(), n < m ? n : m);
+        p.swap(q);
+        cap = c;
+      }
+      n = m;
+    }
+  } buf;
+  size_t carry = 0;          // bytes at the front of buf left from the previous window
+  bool header_done = false;
+  size_t bi = 0;
+  uint64_t kWindow = 256ull << 20;  // SCT_BAM_WINDOW (bytes) shrinks it: tests of the carry path
+  if (const char* w = getenv("SCT_BAM_WINDOW")) kWindow = strtoull(w, nullptr, 10) ? strtoull(w, nullptr, 10) : kWindow;
+  std::vector<z_stream> zs(n_threads);
+  for (auto& z : zs) {
+    memset(&z, 0, sizeof(z));
+    inflateInit2(&z, -15);
+  }
+  struct ZEnd {
+    std::vector<z_stream>& zs;
+    ~ZEnd() {
+      for (auto& z : zs) inflateEnd(&z);
+    }
+  } zend{zs};
+
+  std::vector<uint64_t> starts;
+  int64_t base = 0;
+  while (bi < blocks.size() || carry) {
+    // 1. inflate the next window of blocks behind the carried bytes
+    size_t bj = bi;
+    uint64_t isz = 0;
+    while (bj < blocks.size() && (isz < kWindow || bj == bi)) isz += blocks[bj++].isize;
+    if (bj == bi && carry) return fail(SCT_BAM_EFORMAT, "truncated BAM record at the end of %s", path);
+    std::vector<uint64_t> dst(bj - bi + 1);
+    dst[0] = carry;
+    for (size_t k = bi; k < bj; k++) dst[k - bi + 1] = dst[k - bi] + blocks[k].isize;
+    buf.resize(dst.back());
+    double ti = now();
+    std::atomic<int> bad{0};
+#pragma omp parallel for num_threads(n_threads) schedule(dynamic, 4)
+    for (long k = (long)bi; k < (long)bj; k++) {
+      if (blocks[k].isize && !inflate_block(f, blocks[k], buf.data() + dst[k - bi], zs[omp_get_thread_num()]))
+        bad = 1;
+    }
+    if (bad) return fail(SCT_BAM_EIO, "cannot inflate a BGZF block of %s", path);
+    t_inflate += now() - ti;
+    ti = now();
+    bi = bj;
+    size_t off = 0;
+    const size_t len = buf.size();
+    if (!header_done) {  // magic, text, references (the header is small: in the first window)
+      if (len < 12 || memcmp(buf.data(), "BAM\1", 4) != 0) return fail(SCT_BAM_EFORMAT, "%s is not a BAM file", path);
+      off = 8 + (size_t)rd32(buf.data() + 4);
+      if (off + 4 > len) return fail(SCT_BAM_EFORMAT, "BAM header of %s exceeds the first window", path);
+      const uint32_t n_ref = rd32(buf.data() + off);
+      off += 4;
+      for (uint32_t r = 0; r < n_ref; r++) {
+        if (off + 4 > len) return fail(SCT_BAM_EFORMAT, "BAM header of %s exceeds the first window", path);
+        off += 4 + (size_t)rd32(buf.data() + off) + 4;
+      }
+      header_done = true;
+    }
+    // 2. record starts
+    starts.clear();
+    while (off + 4 <= len) {
+      const uint32_t bs = rd32(buf.data() + off);
+      if (off + 4 + bs > len) break;
+      starts.push_back(off);
+      off += 4 + bs;
+    }
+    if (bi == blocks.size() && off != len) return fail(SCT_BAM_EFORMAT, "truncated BAM record at the end of %s", path);
+    // 3. parse + intern
+    const int64_t nw = (int64_t)starts.size();
+    B->c.resize((size_t)(base + nw));
+    std::atomic<int64_t> first_bad{INT64_MAX};
+    std::mutex err_m;
+    RecErr first_err;
+    Columns& C = B->c;
+#pragma omp parallel num_threads(n_threads)
+    {
+      std::string tmp;
+      Parsed o;
+      RecErr e;
+      std::unique_ptr<TagCache[]> cache(new TagCache[3]);
+#pragma omp for schedule(dynamic, 4096)
+      for (int64_t i = 0; i < nw; i++) {
+        const uint8_t* d = buf.data() + starts[i] + 4;
+        const uint32_t bs = rd32(buf.data() + starts[i]);
+        if (parse_record(d, bs, is_cell, o, e)) {
+          std::lock_guard<std::mutex> lk(err_m);
+          if (base + i < first_bad.load()) {
+            first_bad = base + i;
+            first_err = e;
+          }
+          continue;
+        }
+        const int64_t j = base + i;
+        C.ref[j] = o.ref, C.pos[j] = o.pos;
+        C.gq_sum[j] = (uint16_t)o.gq_sum, C.gq_len[j] = (uint16_t)o.gq_len, C.gq_gt30[j] = (uint16_t)o.gq_gt30;
+        C.bits[j] = o.bits, C.xf[j] = o.xf;
+        C.cy_gt30[j] = (uint8_t)o.cy_gt30, C.cy_len[j] = (uint8_t)o.cy_len;
+        C.uy_gt30[j] = (uint8_t)o.uy_gt30, C.uy_len[j] = (uint8_t)o.uy_len;
+        C.cell[j] = intern_tag(dicts[0], cache[0], o.cb, tmp);
+        C.umi[j] = intern_tag(dicts[1], cache[1], o.ub, tmp);
+        C.gene[j] = intern_tag(dicts[2], cache[2], o.ge, tmp);
+        if (!o.cb.present) has_none[0] = 1;
+        if (!o.ub.present) has_none[1] = 1;
+        if (!o.ge.present) has_none[2] = 1;
+      }
+    }
+    t_parse += now() - ti;
+    if (first_bad.load() != INT64_MAX) {
+      if (bad_record) *bad_record = first_bad.load();
+      return fail(first_err.code, "%s", first_err.msg.c_str());
+    }
+    base += nw;
+    // 4. carry the cut record
+    carry = len - off;
+    if (carry) memmove(buf.data(), buf.data() + off, carry);
+    buf.resize(carry);
+    if (bi == blocks.size() && carry == 0) break;
+  }
+  B->n = base;
+  if (base == 0) return fail(SCT_BAM_EMPTY, "generator raised StopIteration");
+  // 5. rank the dictionaries: sorted strings, the missing value first
+  for (int t = 0; t < 3; t++) {
+    std::vector<std::pair<std::string, int32_t>> all;
+    dicts[t].collect(all);
+    std::sort(all.begin(), all.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    const int32_t hn = has_none[t].load();
+    std::vector<int32_t> rank((size_t)dicts[t].count() + 1, 0);
+    B->has_none[t] = hn;
+    B->dict_off[t].push_back(0);
+    if (hn) B->dict_off[t].push_back(0);
+    for (size_t r = 0; r < all.size(); r++) {
+      rank[all[r].second] = (int32_t)r + hn;
+      B->dict_bytes[t] += all[r].first;
+      B->dict_off[t].push_back((int64_t)B->dict_bytes[t].size());
+    }
+    std::vector<int32_t>& col = t == 0 ? B->c.cell : t == 1 ? B->c.umi : B->c.gene;
+#pragma omp parallel for num_threads(n_threads) schedule(static)
+    for (int64_t i = 0; i < base; i++) col[i] = rank[col[i]];
+  }
+  if (timing)
+    fprintf(stderr, "sct_bam: %lld records, scan %.3fs, inflate %.3fs, parse+intern %.3fs, rank %.3fs (%d threads)\n",
+            (long long)base, t_scan, t_inflate, t_parse, now() - t0 - t_scan - t_inflate - t_parse, n_threads);
+  *out = guard.release();
+  return SCT_BAM_OK;
+}
+
+int64_t sct_bam_n(const sct_bam_t* b) { return b ? b->n : 0; }
+
+const void* sct_bam_column(const sct_bam_t* b, const char* name) {
+  if (!b || !name) return nullptr;
+  const Columns& c = b->c;
+  const std::string s(name);
+  if (s == "cell") return c.cell.data();
+  if (s == "umi") return c.umi.data();
+  if (s == "gene") return c.gene.data();
+  if (s == "ref") return c.ref.data();
+  if (s == "pos") return c.pos.data();
+  if (s == "gq_sum") return c.gq_sum.data();
+  if (s == "gq_len") return c.gq_len.data();
+  if (s == "gq_gt30") return c.gq_gt30.data();
+  if (s == "bits") return c.bits.data();
+  if (s == "xf") return c.xf.data();
+  if (s == "cy_gt30") return c.cy_gt30.data();
+  if (s == "cy_len") return c.cy_len.data();
+  if (s == "uy_gt30") return c.uy_gt30.data();
+  if (s == "uy_len") return c.uy_len.data();
+  return nullptr;
+}
+
+int sct_bam_dictionary(const sct_bam_t* b, int32_t which, int64_t* n, const char** bytes, const int64_t** offsets,
+                       int32_t* has_none) {
+  if (!b || which < 0 || which > 2 || !n || !bytes || !offsets || !has_none)
+    return fail(SCT_BAM_EIO, "bad sct_bam_dictionary arguments");
+  *n = (int64_t)b->dict_off[which].size() - 1;
+  *bytes = b->dict_bytes[which].data();
+  *offsets = b->dict_off[which].data();
+  *has_none = b->has_none[which];
+  return SCT_BAM_OK;
+}
+
+void sct_bam_close(sct_bam_t* b) { delete b; }
+
+}  // extern "C"
