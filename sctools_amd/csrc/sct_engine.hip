@@ -148,13 +148,14 @@ int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool du
     HIPCHK(hipMemsetAsync(seen, 0, sizeof(uint32_t) * (size_t)n_ids, s));
   }
   HIPCHK(hipMemsetAsync(sc, 0, 2 * sizeof(uint64_t), s));
-  LAUNCH("heads", k_heads, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, sc + 1);
+  LAUNCH("heads", k_heads, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, (uint32_t)n_ids, sc + 1);
   LAUNCH("scan", k_scan_wide, dim3(1), dim3(kScanWide), s, tc, tiles, sc);
   uint64_t host[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(host, sc, sizeof(host), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   *n_ent = (int64_t)host[0];
-  if (dup) *dup = host[1] != 0;
+  if (dup) *dup = host[1] & 1;
+  if (host[1] & 2) return fail(SCT_EINVAL, "an entity id lies outside [0, %d)", n_ids);
   return SCT_OK;
 }
 
@@ -205,6 +206,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   BucketCtl h{};
   HIPCHK(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (h.err & 2) return fail(SCT_EINVAL, "a gene / cell / umi id lies outside its dictionary size");
   if (h.err) return 1;
   int depth = 0, level = 1, c = 0;
   while (h.n_seg > 0) {
@@ -343,7 +345,8 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     b.inv = inv & b.k1_mask();
   }
 
-  KeyCols kc{ent_col, cell ? rec->gene : rec->cell, rec->umi};
+  KeyCols kc{ent_col, cell ? rec->gene : rec->cell, rec->umi, (uint32_t)(cell ? plan->n_gene_ids : plan->n_cell_ids),
+             (uint32_t)plan->n_umi_ids};
   RecCols rc2{rec->ref, rec->pos, rec->gq_sum, rec->gq_len, rec->gq_gt30, rec->bits, rec->xf,
               rec->cy_gt30, rec->cy_len, rec->uy_gt30, rec->uy_len};
   SortBuffers B{at<uint64_t>(ws, L.keys_a), at<uint64_t>(ws, L.keys_b), at<uint32_t>(ws, L.vals_a),
@@ -367,9 +370,9 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   const uint64_t* toff = at<uint64_t>(ws, L.tile_cnt);
   // exact mean / variance lanes of the output rows ride along in the same launch
   const bool streams = exact && out_i;
+  BucketCtl* ctl = bucket_ctl(ws, L);
+  HIPCHK(hipMemsetAsync(ctl, 0, sizeof(BucketCtl), s));
   if (bucket) {
-    BucketCtl* ctl = bucket_ctl(ws, L);
-    HIPCHK(hipMemsetAsync(ctl, 0, sizeof(BucketCtl), s));
     uint64_t* va = at<uint64_t>(ws, L.vals_a);
     rc = streams ? launch_build_keys<true, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
                                                  partials, gcounts, L.n_buckets, &ctl->err)
@@ -377,9 +380,14 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
                                                   partials, gcounts, L.n_buckets, &ctl->err);
   } else {
     rc = streams ? launch_build_keys<false, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
-                                                  ent_start, partials, gcounts, L.n_buckets, nullptr)
+                                                  ent_start, partials, gcounts, L.n_buckets, &ctl->err)
                  : launch_build_keys<false, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
-                                                   ent_start, partials, gcounts, L.n_buckets, nullptr);
+                                                   ent_start, partials, gcounts, L.n_buckets, &ctl->err);
+    if (rc) return rc;
+    uint32_t err = 0;  // the bucket path reads the flag at its first level sync
+    HIPCHK(hipMemcpyAsync(&err, &ctl->err, sizeof(err), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (err & 2) return fail(SCT_EINVAL, "a gene / cell / umi id lies outside its dictionary size");
   }
   if (rc) return rc;
 

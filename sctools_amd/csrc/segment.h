@@ -21,9 +21,9 @@ namespace sct {
 
 // heads per tile.  With `seen` set (grouped gene partials), every run head also bumps
 // seen[entity value]; a value seen twice means the column is not sorted into single
-// runs and *dup_flag is raised.
+// runs and *dup_flag gets bit 0; a value outside [0, n_ids) sets bit 1.
 __global__ void k_heads(const int32_t* __restrict__ key, int64_t n, uint64_t* __restrict__ tile_cnt,
-                        uint32_t* __restrict__ seen, uint64_t* __restrict__ dup_flag) {
+                        uint32_t* __restrict__ seen, uint32_t n_ids, uint64_t* __restrict__ dup_flag) {
   const int64_t base = (int64_t)blockIdx.x * kTile;
   uint64_t c = 0;
 #pragma unroll 4
@@ -34,7 +34,8 @@ __global__ void k_heads(const int32_t* __restrict__ key, int64_t n, uint64_t* __
       const bool h = (p == 0 || v != key[p - 1]);
       c += h ? 1 : 0;
       if (h && seen) {
-        if (atomicAdd(&seen[v], 1u) != 0u) atomicOr((unsigned long long*)dup_flag, 1ull);
+        if ((uint32_t)v >= n_ids) atomicOr((unsigned long long*)dup_flag, 2ull);  // id outside the dictionary
+        else if (atomicAdd(&seen[v], 1u) != 0u) atomicOr((unsigned long long*)dup_flag, 1ull);
       }
     }
   }
@@ -53,6 +54,7 @@ struct KeyCols {
   const int32_t* ent;  // column whose runs are the entities
   const int32_t* k1;
   const int32_t* k2;
+  uint32_t n_k1, n_k2;  // dictionary sizes: ids outside them set bit 1 of *err
 };
 
 __device__ __forceinline__ uint64_t make_key(uint64_t e, uint32_t k1, uint32_t k2, uint32_t hash, const Bits& b) {
@@ -237,8 +239,12 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
     wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
     if (!valid) continue;
     cur_e = e;
-    const uint32_t k1 = (uint32_t)c.k1[p];
-    const uint32_t k2 = (uint32_t)c.k2[p];
+    uint32_t k1 = (uint32_t)c.k1[p];
+    uint32_t k2 = (uint32_t)c.k2[p];
+    if (k1 >= c.n_k1 || k2 >= c.n_k2) {  // invalid input: reported, never used as an index
+      atomicOr(err, 2u);
+      k1 = k2 = 0;
+    }
     const uint8_t bt = r.bits[p];
     const uint8_t xf = r.xf[p];
     const bool mapped = !(bt & SCT_B_UNMAPPED);

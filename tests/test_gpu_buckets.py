@@ -1,11 +1,12 @@
 """Edge cases of the bucket path (sctools_amd/csrc/bucket.h) against the oracle.
 
 Records are crafted so that every branch of the MSD partition runs:
-* a k1 value (gene of a cell) with > 2047 reads, split over sibling buckets (k1 split flags);
-* a molecule with > 2047 reads over many positions, split on fragment-hash bits (molecule flags);
-* a molecule with > 2047 reads at ONE fragment: a giant bucket (whole key fixed);
+* a k1 value (gene of a cell) with > 3071 reads, split over sibling buckets (k1 split flags);
+* a molecule with > 3071 reads over many positions, split on fragment-hash bits (molecule flags);
+* a molecule with > 3071 reads at ONE fragment: a giant bucket (whole key fixed);
 * a giant holding two different fragments whose hashes collide in the key's hash bits,
   plus unmapped records (the exact fragment loop);
+* big buckets (1024-3071 records) from level 0 and from a level-1 child;
 * thousands of tiny entities (many buckets per tile);
 both with narrow dictionaries (the k1 boundary inside the first digit) and wide ones.
 The global-sort path (SCT_FORCE_GLOBAL_SORT=1) must give identical rows.
@@ -59,23 +60,33 @@ def craft(n_gene_ids, n_umi_ids, seed):
 
     g_heavy = n_gene_ids - 3
     # cell 0: background + a giant molecule at one fragment + a colliding-hash giant + unmapped reads
+    # (giants: > kBigCap = 3071 records under one fixed key')
     for _ in range(2000):
         add(0, int(rng.integers(1, n_gene_ids)), int(rng.integers(0, n_umi_ids)), int(rng.integers(0, 25)),
             int(rng.integers(0, 1 << 20)))
-    add(0, g_heavy, 5, 1, 1000, k=2600)
+    add(0, g_heavy, 5, 1, 1000, k=4000)
     p2 = colliding_pos(3, 777, hbits)
-    add(0, g_heavy, 6, 3, 777, k=1300)
-    add(0, g_heavy, 6, 3, p2, k=1200)
+    add(0, g_heavy, 6, 3, 777, k=2000)
+    add(0, g_heavy, 6, 3, p2, k=1800)
     add(0, g_heavy, 6, 3, 777, k=1)
     add(0, g_heavy, 6, -1, -1, unmapped=True, k=40)
-    # cell 1: one gene with 5000 reads over 12 UMIs (k1 split) at random positions
-    for _ in range(5000):
+    # cell 1: one gene with 9000 reads over 12 UMIs (k1 split across sibling buckets)
+    for _ in range(9000):
         add(1, 7 % n_gene_ids, int(rng.integers(0, 12)), 2, int(rng.integers(0, 1 << 16)))
-    # cell 2: one molecule with 3000 reads over 400 positions (molecule split on hash bits)
-    for _ in range(3000):
+    # cell 2: one molecule with 5000 reads over 400 positions (molecule split on hash bits)
+    for _ in range(5000):
         add(2, 9 % n_gene_ids, 3, 4, int(rng.integers(0, 400)) * 10)
-    # cells 3..: thousands of tiny cells (1-4 reads)
-    c = 3
+    # cell 3: 2500 reads of one gene over 30 UMIs: a big bucket straight from level 0
+    for _ in range(2500):
+        add(3, 11 % n_gene_ids, int(rng.integers(0, min(30, n_umi_ids))), 5, int(rng.integers(0, 1 << 18)))
+    # cell 4: background + 2800 reads of one gene: a big bucket from a level-1 child
+    for _ in range(2000):
+        add(4, int(rng.integers(1, n_gene_ids)), int(rng.integers(0, n_umi_ids)), int(rng.integers(0, 25)),
+            int(rng.integers(0, 1 << 20)))
+    for _ in range(2800):
+        add(4, 13 % n_gene_ids, int(rng.integers(0, min(200, n_umi_ids))), 6, int(rng.integers(0, 1 << 18)))
+    # cells 5..: thousands of tiny cells (1-4 reads)
+    c = 5
     for _ in range(4000):
         for _ in range(int(rng.integers(1, 5))):
             add(c, int(rng.integers(0, n_gene_ids)), int(rng.integers(0, n_umi_ids)), int(rng.integers(0, 25)),
@@ -170,3 +181,26 @@ def test_global_sort_path_agrees(eng, monkeypatch):
     for k in a:
         assert np.array_equal(a[k][0], b[k][0]), k
         assert np.array_equal(np.nan_to_num(a[k][1], nan=7.0), np.nan_to_num(b[k][1], nan=7.0)), k
+
+
+@pytest.mark.parametrize("column", ["gene", "umi", "cell"])
+def test_ids_outside_the_dictionaries_are_rejected(eng, column):
+    """Invalid input fails loudly (SCT_EINVAL) instead of corrupting keys or indexing tables."""
+    from sctools_amd import _native as N
+    from sctools_amd import engine as E
+
+    arrays, mito, n_cells = craft(300, 4096, 4)
+    arrays = {k: v.copy() for k, v in arrays.items()}
+    limit = {"gene": 300, "umi": 4096, "cell": n_cells}[column]
+    arrays[column][len(arrays[column]) // 2] = limit + 5
+    dims = E.Dims(n_cells, 300, 4096)
+    cols = E.to_device(arrays, eng.device)
+    gm = torch.from_numpy(mito).to(eng.device)
+    if column == "cell":  # the cell id indexes the grouped-partials duplicate check
+        with pytest.raises(N.EngineError, match="outside"):
+            eng.cell_and_gene(cols, dims, gm)
+    else:
+        with pytest.raises(N.EngineError, match="outside"):
+            eng.compute(cols, "cell", dims, gm, gm, float_mode="exact")
+        with pytest.raises(N.EngineError, match="outside"):
+            eng.cell_and_gene(cols, dims, gm)
