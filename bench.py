@@ -72,9 +72,10 @@ def parse():
     ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="target seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
-                    help="2: cell-sorted records (default); 5: globally shuffled records, 30%% NH>1, 40%% duplicates, "
-                         "sorted by cell on the GPU inside every step (SURVEY.md 8(d) config 5)")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5],
+                    help="2: cell-sorted records (default); 4: the 1B-read atlas per GPU of 8 -- 125M records, 62.5k "
+                         "cells with lognormal(0, 2) reads; 5: globally shuffled records, 30%% NH>1, 40%% duplicates, "
+                         "sorted by cell on the GPU inside every step (SURVEY.md 8(d) configs 4, 5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"),
                     help="rocprofv3 --pmc per-kernel HBM bytes (tools/pmc_passes.sh) for roofline.traffic")
     return ap.parse_args()
@@ -103,8 +104,10 @@ def main():
 
     eng = E.get_engine(dev)
     t0 = time.time()
-    cfg = synth.SynthConfig(n_reads=args.records, n_cells=args.cells, n_genes=args.genes, sigma=1.0,
-                            seed=args.seed + 1000 * rank)
+    if args.config == 4:
+        args.records, args.cells = 125_000_000, 62_500
+    cfg = synth.SynthConfig(n_reads=args.records, n_cells=args.cells, n_genes=args.genes,
+                            sigma=2.0 if args.config == 4 else 1.0, seed=args.seed + 1000 * rank)
     if args.config == 5:
         cfg.p_nh1, cfg.p_dup = 0.70, 0.40
     data = synth.generate(cfg, device=dev, chunk=16_000_000)
@@ -226,9 +229,10 @@ def main():
             "dtype": "int64",
             "data": "synthetic (SURVEY.md 8(d) config-2 generator, generated on GPU)",
             "config": {
-                "workload": ("config2: %d cell-sorted records/rank" if args.config == 2 else
-                             "config5: %d globally shuffled records/rank (30%% NH>1, 40%% dup), GPU sort by cell + ")
-                            % args.records + ", %d cells/rank, %d genes; cell metrics + grouped gene metrics%s"
+                "workload": ({2: "config2: %d cell-sorted records/rank",
+                              4: "config4: %d cell-sorted records/rank, lognormal(0, 2) reads per cell",
+                              5: "config5: %d globally shuffled records/rank (30%% NH>1, 40%% dup), GPU sort by cell + "}
+                             [args.config]) % args.records + ", %d cells/rank, %d genes; cell metrics + grouped gene metrics%s"
                             % (args.cells, args.genes, " + RCCL all-reduce" if world > 1 else ""),
                 "records_per_rank": args.records,
                 "cells_per_rank": args.cells,
@@ -305,7 +309,7 @@ def cpu_baseline(data, args):
         "cores": threads,
         "kind": "port",
         "sample": ("first %d records (%d whole cells) of rank 0's shard: oracle cell metrics + grouped gene "
-                   "metrics, %.1fs" % (n1, int(h1["cell"][-1]) + 1, t1)) if args.config == 2 else
+                   "metrics, %.1fs" % (n1, int(h1["cell"][-1]) + 1, t1)) if args.config != 5 else
                   ("first %d records of rank 0's shuffled shard: numpy stable sort by cell + oracle cell metrics + "
                    "grouped gene metrics, %.1fs" % (n1, t1)),
     }
