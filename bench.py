@@ -40,7 +40,9 @@ ALG_BYTES = {
     "big_bucket": 18,        # read payload w0 + w1 (16) of the big buckets' records, write dflags (2)
     "gene_emit": 32,         # read gene/bits/xf/dflags/uy/gq (16), write 16-byte gene payload
     "gene_reduce": 16,       # read the 16-byte gene payload
-    "tag_pack": 64,          # config 5: read the 32-byte SoA record, write it packed
+    "tag_row_scatter": 68,   # config 5, per pass: read a 32-byte row (SoA or packed), write it (+ 4-byte key)
+    "tag_row_hist": 4,       # config 5, per pass: read the cell key
+    "tag_pack": 64,          # tag sort with a tiebreak: read the 32-byte SoA record, write it packed
     "tag_keys": 28,          # read the packed record's key words (16), write key 8 + index 4
     "tag_unpack": 64,        # gather the packed record (32), write the SoA columns (32)
     "radix_downsweep": 24,   # global-sort path: read key 8 + value 4, write key 8 + value 4

@@ -451,13 +451,13 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
 
 // ---- tag sort ----
 struct SortLayout {
-  size_t recs, ka, kb, va, vb, counts, offsets, sums, bad, total;
+  size_t recs, recs2, ka, kb, va, vb, counts, offsets, sums, bad, total;
 };
 
 SortLayout sort_layout(int64_t n) {
   SortLayout L;
   const int64_t n1 = n > 0 ? n : 1;
-  const int64_t tiles = cdiv(n1, kTile);
+  const int64_t tiles = cdiv(n1, kRowTile);  // row passes use the smaller tiles
   const int64_t m = (int64_t)kRadix * tiles;
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -466,6 +466,7 @@ SortLayout sort_layout(int64_t n) {
     return o;
   };
   L.recs = take(sizeof(PackedRec) * (size_t)n1);
+  L.recs2 = take(sizeof(PackedRec) * (size_t)n1);
   L.ka = take(sizeof(uint64_t) * (size_t)n1);
   L.kb = take(sizeof(uint64_t) * (size_t)n1);
   L.va = take(sizeof(uint32_t) * (size_t)n1);
@@ -663,6 +664,41 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
     return fail(SCT_ENOMEM, "workspace too small (%zu < %zu)", workspace_bytes, L.total);
   hipStream_t s = (hipStream_t)stream;
   uint4* recs = at<uint4>(workspace, L.recs);
+  if (order == SCT_ORDER_CELL && !tiebreak) {  // whole rows through 8-bit LSD passes, no gathers
+    const int bits = f[0].bits;
+    const int passes = bits > kRadixBits ? (bits + kRadixBits - 1) / kRadixBits : 1;
+    const int64_t tiles = cdiv(n, kRowTile);
+    uint32_t* counts = at<uint32_t>(workspace, L.counts);
+    uint32_t* offsets = at<uint32_t>(workspace, L.offsets);
+    uint64_t* sums = at<uint64_t>(workspace, L.sums);
+    uint4* rows[2] = {recs, at<uint4>(workspace, L.recs2)};
+    int32_t* keys[2] = {at<int32_t>(workspace, L.ka), at<int32_t>(workspace, L.kb)};
+    for (int ps = 0; ps < passes; ps++) {
+      const int shift = ps * kRadixBits;
+      const bool first = ps == 0, last = ps == passes - 1;
+      const int32_t* hkey = first ? in->cell : keys[(ps - 1) & 1];
+      LAUNCH("tag_row_hist", k_row_hist, dim3((unsigned)tiles), dim3(kBlock), s, hkey, n, shift, tiles, counts);
+      rc = scan_counts(counts, (int64_t)kRadix * tiles, offsets, sums, s);
+      if (rc) return rc;
+      const uint4* rin = first ? nullptr : rows[(ps - 1) & 1];
+      uint4* rout = rows[ps & 1];
+      int32_t* kout = keys[ps & 1];
+#define SCT_ROWS(A, Z)                                                                                              \
+  LAUNCH("tag_row_scatter", (k_row_scatter<A, Z>), dim3((unsigned)tiles), dim3(kBlock), s, *in, rin, rout, kout, \
+         *out, n, shift, tiles, (const uint32_t*)offsets)
+      if (first && last) {
+        SCT_ROWS(true, true);
+      } else if (first) {
+        SCT_ROWS(true, false);
+      } else if (last) {
+        SCT_ROWS(false, true);
+      } else {
+        SCT_ROWS(false, false);
+      }
+#undef SCT_ROWS
+    }
+    return SCT_OK;
+  }
   SortBuffers B{at<uint64_t>(workspace, L.ka), at<uint64_t>(workspace, L.kb), at<uint32_t>(workspace, L.va),
                 at<uint32_t>(workspace, L.vb), at<uint32_t>(workspace, L.counts), at<uint32_t>(workspace, L.offsets),
                 at<uint64_t>(workspace, L.sums)};

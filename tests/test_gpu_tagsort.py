@@ -184,3 +184,17 @@ def test_unsorted_input_cell_metrics_after_gpu_sort(eng):
     assert np.array_equal(ci0[:, keep], ci1[:, keep])
     assert np.array_equal(np.nan_to_num(cf0, nan=-7.0), np.nan_to_num(cf1, nan=-7.0))
     assert torch.equal(p0, p1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_cell_ids", [200, 1 << 12, 1 << 20])
+def test_cell_order_row_passes(eng, n_cell_ids):
+    """Cell order without a tiebreak moves whole rows through 1, 2 or 3 LSD passes."""
+    from sctools_amd import engine as E
+
+    d, _, arrays = shuffled_synth(300_000, 8, n_cells=150)
+    dims = E.Dims(max(n_cell_ids, d.n_cell_ids), d.n_gene_ids, d.n_umi_ids)
+    out = to_host(eng.tag_sort(to_dev(eng, arrays), dims, "cell"))
+    idx = np_order(arrays, "cell")
+    for c in N.RECORD_COLUMNS:
+        assert np.array_equal(out[c], arrays[c][idx]), c
