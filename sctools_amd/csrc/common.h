@@ -86,6 +86,6 @@ struct __attribute__((aligned(16))) GenePayload {
 static_assert(sizeof(GenePayload) == 16, "gene payload must be 16 bytes");
 
 constexpr int kGenesPerBucket = 64;  // LDS bins of one gene bucket
-constexpr int kMaxGeneBuckets = 2048;  // n_gene_ids <= 131072
+constexpr int kMaxGeneBuckets = 4096;  // n_gene_ids <= 262144 (gene-bucket arrays in dynamic LDS, <= 64 KB a block)
 
 }  // namespace sct

@@ -90,8 +90,8 @@ __global__ void __launch_bounds__(kBlock) k_gene_emit(const int32_t* __restrict_
                                                       const uint16_t* __restrict__ dflags, int64_t n,
                                                       uint32_t* __restrict__ cursor, int n_buckets,
                                                       GenePayload* __restrict__ pay) {
-  __shared__ uint32_t s_cnt[kMaxGeneBuckets];
-  __shared__ uint32_t s_off[kMaxGeneBuckets];
+  uint32_t* s_cnt = sct_dyn_lds;              // n_buckets (dynamic LDS)
+  uint32_t* s_off = sct_dyn_lds + n_buckets;  // n_buckets
   __shared__ uint16_t s_rank[kEmitTile];
   const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * kEmitTile;
@@ -132,8 +132,8 @@ __global__ void __launch_bounds__(kBlock) k_gene_plan(const uint32_t* __restrict
                                                       uint32_t* __restrict__ cursor, int64_t* __restrict__ work,
                                                       int64_t* __restrict__ n_work) {
   __shared__ uint64_t lds[kWaves + 1];
-  __shared__ uint32_t s_beg[kMaxGeneBuckets + 1];
-  __shared__ uint32_t s_woff[kMaxGeneBuckets + 1];
+  uint32_t* s_beg = sct_dyn_lds;                   // n_buckets + 1 (dynamic LDS)
+  uint32_t* s_woff = sct_dyn_lds + n_buckets + 1;  // n_buckets + 1
   uint64_t carry = 0, carry_w = 0;
   for (int base = 0; base < n_buckets; base += kBlock) {
     const int bk = base + threadIdx.x;

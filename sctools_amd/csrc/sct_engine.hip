@@ -283,8 +283,9 @@ int launch_build_keys(bool cell, bool gene, dim3 grid, hipStream_t s, const KeyC
                       void* vals, int64_t* ent_start, int64_t* partials, uint32_t* gcounts, int n_buckets,
                       uint32_t* err) {
   if (cell && gene) {
-    LAUNCH("build_keys", (k_build_keys_run<true, true, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito, n,
-           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err);
+    LAUNCH_SHM("build_keys", (k_build_keys_run<true, true, kBucket, kStreams>), grid, dim3(kBlock),
+               sizeof(uint32_t) * (size_t)n_buckets, s, kc, rc2, mito, n, toff, b, keys, vals, ent_start, partials,
+               gcounts, n_buckets, err);
   } else if (cell) {
     LAUNCH("build_keys", (k_build_keys_run<true, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito, n,
            toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err);
@@ -437,10 +438,11 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     int64_t* gwork = at<int64_t>(ws, L.gwork);
     int64_t* n_gwork = at<int64_t>(ws, L.scalars) + 4;
     GenePayload* gpay = at<GenePayload>(ws, L.gpay);
-    LAUNCH("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), s, (const uint32_t*)gcounts, L.n_buckets, gcur, gwork,
-           n_gwork);
-    LAUNCH("gene_emit", k_gene_emit, dim3((unsigned)cdiv(n, kEmitTile)), dim3(kBlock), s, rec->gene, rc2,
-           (const uint16_t*)dflags, n, gcur, L.n_buckets, gpay);
+    LAUNCH_SHM("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), 2 * sizeof(uint32_t) * (size_t)(L.n_buckets + 1), s,
+               (const uint32_t*)gcounts, L.n_buckets, gcur, gwork, n_gwork);
+    LAUNCH_SHM("gene_emit", k_gene_emit, dim3((unsigned)cdiv(n, kEmitTile)), dim3(kBlock),
+               2 * sizeof(uint32_t) * (size_t)L.n_buckets, s, rec->gene, rc2, (const uint16_t*)dflags, n, gcur,
+               L.n_buckets, gpay);
     HIPCHK(hipMemsetAsync(gene_partials, 0, sizeof(int64_t) * SCT_NP * (size_t)plan->n_gene_ids, s));
     LAUNCH("gene_reduce", k_gene_reduce, dim3((unsigned)L.max_gene_work), dim3(kBlock), s, (const GenePayload*)gpay,
            (const int64_t*)gwork, (const int64_t*)n_gwork, plan->n_gene_ids, gene_partials);

@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
   __shared__ int32_t s_e[kTile];
   __shared__ int32_t s_prev;
   __shared__ uint64_t s_scan[kWaves + 1];
-  __shared__ uint32_t s_hist[kGene ? kMaxGeneBuckets : 1];
+  uint32_t* s_hist = sct_dyn_lds;  // kGene: n_buckets counters (dynamic LDS)
   __shared__ double s_rcp[kStreams ? kRcpN : 1];
   const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * kTile;

@@ -83,6 +83,14 @@ struct ProfScope {
   } while (0);                                                   \
   LAUNCHCHK()
 
+// with `shm` bytes of dynamic LDS (sct_dyn_lds)
+#define LAUNCH_SHM(name, kern, grid, block, shm, strm, ...)        \
+  do {                                                             \
+    ::sct::ProfScope _ps(name, strm);                              \
+    hipLaunchKernelGGL(kern, grid, block, shm, strm, __VA_ARGS__); \
+  } while (0);                                                     \
+  LAUNCHCHK()
+
 inline int bitlen(uint64_t v) {  // bits for ids 0..v-1; 0 when v <= 1
   return v <= 1 ? 0 : 64 - __builtin_clzll(v - 1);
 }
@@ -95,6 +103,8 @@ inline T* at(void* ws, size_t off) {
 }
 
 // ---------------- device helpers ----------------
+// dynamic LDS of a launch (sized per launch: gene-bucket arrays follow the dictionary size)
+extern __shared__ uint32_t sct_dyn_lds[];
 constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, each with its own (non-coherent) 4 MiB L2
 
 // Workgroups are dispatched round-robin over the XCDs (block b -> XCD b % 8).  Map them to

@@ -120,6 +120,7 @@ def compare(gi, gf, oi, of, exact_floats):
     (22, 2_000_000, 200, 30_000, 1.0),
     (23, 1_500_000, 2_000, 5_000, 2.0),
     (24, 8_000_000, 100, 30_000, 2.0),  # heavy tail: cells of 10^5-10^6 reads, several partition levels
+    (25, 1_000_000, 300, 100_000, 1.0),  # 200,001 gene ids: more gene buckets than 2048 (dynamic LDS)
 ])
 def test_gpu_generated_against_oracle(eng, seed, n, cells, genes, sigma):
     from sctools_amd import engine as E
