@@ -58,10 +58,7 @@ constexpr int kNarrowK1Bits = 32 - 2 - kWinBits;  // k1 ids up to 20 bits use a 
 // big buckets: kBCap < records <= kBigCap, one kBigBlock-thread block each with kBigSlots-slot
 // tables (load factor <= 3/4).  Typically a hot gene's records in one cell: taking them here
 // instead of splitting them further on the umi bits saves whole partition levels.
-#ifndef SCT_BIG_BLOCK
-#define SCT_BIG_BLOCK 1024
-#endif
-constexpr int kBigBlock = SCT_BIG_BLOCK;
+constexpr int kBigBlock = 1024;  // measured: 1024 threads 0.38 ms, 512 0.49, 256 0.76 at config 2
 constexpr int kBigBits = 12;
 constexpr int kBigSlots = 1 << kBigBits;
 constexpr int kBigCap = 3 * kBigSlots / 4 - 1;  // 3071

@@ -22,10 +22,7 @@
 namespace sct {
 
 constexpr int kGeneChunk = 16384;  // payloads per reduce block
-#ifndef SCT_GENE_SUB
-#define SCT_GENE_SUB 2048
-#endif
-constexpr int kGeneSub = SCT_GENE_SUB;  // payloads sorted in LDS at a time
+constexpr int kGeneSub = 2048;  // payloads sorted in LDS at a time
 constexpr int kGeneItems = kGeneSub / kBlock;
 constexpr int kGeneCnt = 1 + kGeneFlags;  // n_reads + flag counts (32-bit bins)
 constexpr int kGeneCntPad = 16;
