@@ -6,14 +6,18 @@ SRC := sctools_amd/csrc/sct_engine.hip
 HDRS := $(wildcard sctools_amd/csrc/*.h) include/sctools_gpu.h
 
 BAMDEC := sctools_amd/libsct_bam.so
+CSVFMT := sctools_amd/libsct_csv.so
 
-all: $(ENGINE) $(BAMDEC) oracle/liboracle.so tests/native/libfxcheck.so
+all: $(ENGINE) $(BAMDEC) $(CSVFMT) oracle/liboracle.so tests/native/libfxcheck.so
 
 $(ENGINE): $(SRC) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC)
 
 $(BAMDEC): sctools_amd/csrc/bamdec.cpp include/sct_bam.h
 	g++ -O3 -std=c++17 -fopenmp -fPIC -shared -Wall -o $@ sctools_amd/csrc/bamdec.cpp -lz
+
+$(CSVFMT): sctools_amd/csrc/csvfmt.cpp include/sct_csv.h
+	g++ -O3 -std=c++17 -fopenmp -fPIC -shared -Wall -o $@ sctools_amd/csrc/csvfmt.cpp -lz
 
 oracle/liboracle.so: oracle/sct_oracle.c include/sctools_gpu.h
 	$(MAKE) -s -C oracle liboracle.so
@@ -22,6 +26,6 @@ tests/native/libfxcheck.so: tests/native/fxcheck.cpp sctools_amd/csrc/fixedpt.h
 	g++ -O2 -std=c++17 -ffp-contract=off -fPIC -shared -o $@ tests/native/fxcheck.cpp
 
 clean:
-	rm -f $(ENGINE) $(BAMDEC) oracle/liboracle.so tests/native/libfxcheck.so
+	rm -f $(ENGINE) $(BAMDEC) $(CSVFMT) oracle/liboracle.so tests/native/libfxcheck.so
 
 .PHONY: all clean

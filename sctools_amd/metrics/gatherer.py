@@ -51,7 +51,7 @@ def write_rows(writer: MetricCSVWriter, mode: str, cols: columnar.Columns, ints:
     names_of = cols.cells.names if mode == "cell" else cols.genes.names
     names = [names_of[key[i]] for i in ints[:, N.I_ENTITY]]
     keep, kept = R.select_rows(mode, ints, names)
-    writer.write_rows(R.format_rows(mode, kept, ints[keep], floats[keep]))
+    writer.write_bytes(R.format_rows_bytes(mode, kept, ints[keep], floats[keep]))
 
 
 class MetricGatherer:

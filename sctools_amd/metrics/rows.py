@@ -92,6 +92,19 @@ def format_rows(mode: str, names: Sequence, ints: np.ndarray, floats: np.ndarray
         yield entity_name(name) + "," + ",".join([str(c[r]) for c in per_col]) + "\n"
 
 
+def format_rows_bytes(mode: str, names: Sequence, ints: np.ndarray, floats: np.ndarray) -> bytes:
+    """All CSV lines as UTF-8 bytes: the native formatter (libsct_csv.so, all cores, the same text
+    as format_rows) when it is built, else format_rows."""
+    from sctools_amd import csvnative
+
+    if not csvnative.available():
+        return "".join(format_rows(mode, names, ints, floats)).encode("utf-8")
+    cols = columns_for(mode)
+    kinds = [csvnative.INT if kind == I else csvnative.FLOAT for _, kind, _ in cols]
+    slots = [slot for _, _, slot in cols]
+    return csvnative.format_rows([entity_name(n) for n in names], kinds, slots, ints, floats)
+
+
 def select_rows(mode: str, ints: np.ndarray, entity_names: Sequence[Optional[str]],
                 gene_is_multi: Optional[np.ndarray] = None):
     """Row indices to emit and their entity names.
