@@ -33,6 +33,9 @@ extern "C" {
 
 #define SCT_BAM_CELL_METRICS 0 /* require CY (and CR where CB is present), as CellMetrics does   */
 #define SCT_BAM_GENE_METRICS 1 /* records of multi-gene GE values are not validated (gatherer.py:210-212) */
+#define SCT_BAM_COUNT_MATRIX 2 /* CountMatrix.from_sorted_tagged_bam (count.py:134-328): only the cell /
+                                * molecule / gene tags, XF and the query name are read, nothing is
+                                * validated, an empty file is 0 records, and the "qhead" column is set */
 
 #define SCT_BAM_TAG_CB 0
 #define SCT_BAM_TAG_UB 1
@@ -46,6 +49,12 @@ typedef struct sct_bam sct_bam_t;
 int sct_bam_decode(const char* path, int32_t metric_mode, int32_t n_threads, sct_bam_t** out,
                    int64_t* bad_record);
 
+/* As sct_bam_decode, with the three dictionary tags named by `tags` (6 characters: cell,
+ * molecule, gene tag, e.g. "CBUBGE" -- the CreateCountMatrix -c / -m / -g options,
+ * platform.py:402-429).  The metric modes require "CBUBGE". */
+int sct_bam_decode_tags(const char* path, int32_t metric_mode, const char* tags, int32_t n_threads,
+                        sct_bam_t** out, int64_t* bad_record);
+
 /* Message of the calling thread's last error ("" if none). */
 const char* sct_bam_last_error(void);
 
@@ -54,7 +63,9 @@ int64_t sct_bam_n(const sct_bam_t* b);
 
 /* Host pointer to a column by name (the sct_records_t field names: "cell", "umi", "gene",
  * "ref", "pos", "gq_sum", "gq_len", "gq_gt30", "bits", "xf", "cy_gt30", "cy_len",
- * "uy_gt30", "uy_len"); NULL for an unknown name.  Valid until sct_bam_close. */
+ * "uy_gt30", "uy_len"), or "qhead" (uint8: 1 where the record's query name differs from the
+ * previous record's -- the itertools.groupby of count.py:83-86 -- SCT_BAM_COUNT_MATRIX only);
+ * NULL for an unknown name.  Valid until sct_bam_close. */
 const void* sct_bam_column(const sct_bam_t* b, const char* name);
 
 /* Dictionary of tag `which` (SCT_BAM_TAG_*): *n entries in id order; entry i is the UTF-8

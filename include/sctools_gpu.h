@@ -242,6 +242,46 @@ int sct_verify_sort(const sct_plan_t* plan, const sct_records_t* rec, const int3
                     int32_t order, void* workspace, size_t workspace_bytes,
                     int64_t* first_violation /* host */, void* stream);
 
+/* ---- count matrix (CountMatrix.from_sorted_tagged_bam, count.py:134-328) ---- */
+
+#define SCT_COUNT_SKIP (-1)    /* gene_col: never counted (missing tag, or a multi-gene "a,b" value) */
+#define SCT_COUNT_UNKNOWN (-2) /* gene_col: a single gene name outside the annotation (KeyError) */
+
+typedef struct sct_count_input {
+  int64_t n;            /* records, in file order */
+  const int32_t* cell;  /* device, dictionary ids of the cell / molecule / gene tags */
+  const int32_t* umi;
+  const int32_t* gene;
+  const uint8_t* xf;    /* device, SCT_XF_* */
+  const uint8_t* qhead; /* device, 1 where the query name differs from the previous record's */
+  int32_t n_cell_ids, n_umi_ids, n_gene_ids;
+  int32_t cell_none, umi_none; /* id of a missing cell / molecule tag, or -1 */
+  const int32_t* gene_col;     /* device [n_gene_ids]: matrix column, SCT_COUNT_SKIP or SCT_COUNT_UNKNOWN */
+  int32_t n_cols;              /* annotation genes (matrix columns) */
+} sct_count_input_t;
+
+typedef struct sct_count_output {
+  int32_t* row_cell;  /* device [n_cell_ids]: cell id of each row, rows in order of each cell's first counted molecule */
+  int32_t* indptr;    /* device [n_cell_ids + 1]: CSR row pointers (n_rows + 1 written) */
+  int32_t* indices;   /* device [n]: CSR column indices, ascending within a row */
+  uint32_t* data;     /* device [n]: molecules (distinct molecule barcodes) per (cell, gene) */
+  int64_t n_rows;     /* host, set on return */
+  int64_t nnz;        /* host, set on return */
+  int64_t unknown_record; /* host: first record (file order) of a counted molecule whose gene is
+                           * SCT_COUNT_UNKNOWN -- the reference's KeyError -- or -1 */
+} sct_count_output_t;
+
+/* Device workspace bytes for sct_count_matrix. */
+int sct_count_matrix_workspace_size(const sct_count_input_t* in, size_t* bytes);
+
+/* The cells x genes molecule-count matrix in CSR form, as the reference builds it: records
+ * are grouped by runs of equal query name; a group counts when its first record has both
+ * barcodes and exactly one distinct single gene name is carried by its alignments with an
+ * XF tag other than INTERGENIC; a (cell, molecule, gene) triple counts once.  On
+ * unknown_record >= 0 the matrix outputs are not written.  Synchronizes `stream`. */
+int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
 /* Optional kernel timing: while enabled, every kernel launch is bracketed by
  * HIP events on its launch stream.  sct_profile_read waits for the events,
  * fills up to `max_kernels` (name, total ms, launches) triples (host arrays;

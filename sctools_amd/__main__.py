@@ -1,5 +1,5 @@
 """python -m sctools_amd <Command> [args]  (CalculateCellMetrics, CalculateGeneMetrics,
-MergeCellMetrics, MergeGeneMetrics)."""
+MergeCellMetrics, MergeGeneMetrics, CreateCountMatrix, MergeCountMatrices)."""
 import sys
 
 from sctools_amd.platform import COMMANDS

@@ -35,7 +35,7 @@ RECORD_COLUMNS = ("cell", "umi", "gene", "ref", "pos", "gq_sum", "gq_len", "gq_g
 EXPORTED = ("sct_abi_version", "sct_last_error", "sct_workspace_size", "sct_count_entities",
             "sct_compute_metrics", "sct_gene_partials", "sct_cell_metrics_gene_partials",
             "sct_finalize_partials", "sct_profile_enable", "sct_profile_read", "sct_tag_sort_workspace_size",
-            "sct_tag_sort", "sct_verify_sort")
+            "sct_tag_sort", "sct_verify_sort", "sct_count_matrix_workspace_size", "sct_count_matrix")
 ORDER_CELL, ORDER_CELL_UMI_GENE, ORDER_GENE_CELL_UMI = 0, 1, 2
 PLAN_GENE_PARTIALS = 0x1
 
@@ -54,6 +54,39 @@ class Plan(ctypes.Structure):
         ("n_gene_ids", ctypes.c_int32),
         ("n_umi_ids", ctypes.c_int32),
         ("flags", ctypes.c_int32),
+    ]
+
+
+COUNT_SKIP, COUNT_UNKNOWN = -1, -2
+
+
+class CountInput(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int64),
+        ("cell", ctypes.c_void_p),
+        ("umi", ctypes.c_void_p),
+        ("gene", ctypes.c_void_p),
+        ("xf", ctypes.c_void_p),
+        ("qhead", ctypes.c_void_p),
+        ("n_cell_ids", ctypes.c_int32),
+        ("n_umi_ids", ctypes.c_int32),
+        ("n_gene_ids", ctypes.c_int32),
+        ("cell_none", ctypes.c_int32),
+        ("umi_none", ctypes.c_int32),
+        ("gene_col", ctypes.c_void_p),
+        ("n_cols", ctypes.c_int32),
+    ]
+
+
+class CountOutput(ctypes.Structure):
+    _fields_ = [
+        ("row_cell", ctypes.c_void_p),
+        ("indptr", ctypes.c_void_p),
+        ("indices", ctypes.c_void_p),
+        ("data", ctypes.c_void_p),
+        ("n_rows", ctypes.c_int64),
+        ("nnz", ctypes.c_int64),
+        ("unknown_record", ctypes.c_int64),
     ]
 
 
@@ -103,6 +136,10 @@ def load() -> ctypes.CDLL:
     L.sct_verify_sort.restype = ctypes.c_int
     L.sct_verify_sort.argtypes = [ctypes.POINTER(Plan), ctypes.POINTER(Records), vp, i32, vp, ctypes.c_size_t,
                                   ctypes.POINTER(ctypes.c_int64), vp]
+    L.sct_count_matrix_workspace_size.restype = ctypes.c_int
+    L.sct_count_matrix_workspace_size.argtypes = [ctypes.POINTER(CountInput), ctypes.POINTER(ctypes.c_size_t)]
+    L.sct_count_matrix.restype = ctypes.c_int
+    L.sct_count_matrix.argtypes = [ctypes.POINTER(CountInput), ctypes.POINTER(CountOutput), vp, ctypes.c_size_t, vp]
     L.sct_profile_enable.restype = ctypes.c_int
     L.sct_profile_enable.argtypes = [ctypes.c_int]
     L.sct_profile_read.restype = ctypes.c_int

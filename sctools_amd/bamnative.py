@@ -20,8 +20,9 @@ LIB_PATH = os.path.join(HERE, "libsct_bam.so")
 
 OK, EIO, EFORMAT = 0, -1, -2
 KEYERROR, TYPEERROR, ZERODIV, VALUEERROR, EMPTY = -10, -11, -12, -13, -14
-CELL_METRICS, GENE_METRICS = 0, 1
-EXPORTED = ("sct_bam_decode", "sct_bam_last_error", "sct_bam_n", "sct_bam_column", "sct_bam_dictionary",
+CELL_METRICS, GENE_METRICS, COUNT_MATRIX = 0, 1, 2
+_MODES = {"cell": CELL_METRICS, "gene": GENE_METRICS, "count": COUNT_MATRIX}
+EXPORTED = ("sct_bam_decode", "sct_bam_decode_tags", "sct_bam_last_error", "sct_bam_n", "sct_bam_column", "sct_bam_dictionary",
             "sct_bam_close")
 
 _lib: Optional[ctypes.CDLL] = None
@@ -38,6 +39,9 @@ def load() -> ctypes.CDLL:
     L.sct_bam_decode.restype = ctypes.c_int
     L.sct_bam_decode.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(vp),
                                  ctypes.POINTER(ctypes.c_int64)]
+    L.sct_bam_decode_tags.restype = ctypes.c_int
+    L.sct_bam_decode_tags.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
+                                      ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64)]
     L.sct_bam_last_error.restype = ctypes.c_char_p
     L.sct_bam_last_error.argtypes = []
     L.sct_bam_n.restype = ctypes.c_int64
@@ -61,22 +65,30 @@ _EXC = {KEYERROR: KeyError, TYPEERROR: TypeError, ZERODIV: ZeroDivisionError, VA
         EMPTY: RuntimeError, EFORMAT: ValueError, EIO: OSError}
 
 
-def decode(path: str, metric_mode: str = "cell", threads: int = 0):
-    """(arrays, [cell names, umi names, gene names]) -- names in id order, None first if present."""
+def decode(path: str, metric_mode: str = "cell", threads: int = 0, tags=("CB", "UB", "GE")):
+    """(arrays, [cell names, umi names, gene names]) -- names in id order, None first if present.
+
+    metric_mode "count" (CountMatrix): only cell / umi / gene / xf are meaningful, the three
+    dictionary tags are ``tags``, nothing is validated, and ``arrays["qhead"]`` marks the first
+    record of each run of equal query names."""
     from sctools_amd.columnar import COLUMNS
 
     L = load()
     h = ctypes.c_void_p()
     bad = ctypes.c_int64(-1)
-    rc = L.sct_bam_decode(os.fsencode(path), CELL_METRICS if metric_mode == "cell" else GENE_METRICS,
-                          int(threads), ctypes.byref(h), ctypes.byref(bad))
+    tag_bytes = "".join(tags).encode()
+    if len(tag_bytes) != 6 or any(len(t) != 2 for t in tags):
+        raise ValueError("tags must be three two-character BAM tag names: %r" % (tags,))
+    rc = L.sct_bam_decode_tags(os.fsencode(path), _MODES[metric_mode], tag_bytes, int(threads), ctypes.byref(h),
+                               ctypes.byref(bad))
     if rc != OK:
         msg = L.sct_bam_last_error().decode("utf-8", "replace")
         raise _EXC.get(rc, RuntimeError)(msg)
     try:
         n = int(L.sct_bam_n(h))
         arrays = {}
-        for name, dt in COLUMNS:
+        cols = list(COLUMNS) + ([("qhead", np.uint8)] if metric_mode == "count" else [])
+        for name, dt in cols:
             ptr = L.sct_bam_column(h, name.encode())
             buf = (ctypes.c_char * (n * np.dtype(dt).itemsize)).from_address(ptr) if n else b""
             arrays[name] = np.frombuffer(buf, dtype=dt, count=n).copy()

@@ -193,6 +193,7 @@ struct Columns {
   std::vector<int32_t> cell, umi, gene, ref, pos;
   std::vector<uint16_t> gq_sum, gq_len, gq_gt30;
   std::vector<uint8_t> bits, xf, cy_gt30, cy_len, uy_gt30, uy_len;
+  std::vector<uint8_t> qhead;  // count-matrix mode only
   void resize(size_t n) {
     cell.resize(n), umi.resize(n), gene.resize(n), ref.resize(n), pos.resize(n);
     gq_sum.resize(n), gq_len.resize(n), gq_gt30.resize(n);
@@ -492,6 +493,57 @@ int parse_record(const uint8_t* d, uint32_t bs, bool is_cell, Parsed& o, RecErr&
   return 0;
 }
 
+// Count-matrix mode: the three dictionary tags (names in `tags`), XF and the query name; no
+// validation (count.py:222-270 reads only these, through has_tag / get_tag_or_default).
+int parse_count_record(const uint8_t* d, uint32_t bs, const char* tags, Parsed& o, const char** qname,
+                       uint32_t* qlen, RecErr& e) {
+  if (bs < 32) {
+    e.code = SCT_BAM_EFORMAT;
+    e.msg = "truncated BAM record";
+    return -1;
+  }
+  const uint32_t l_read_name = d[8];
+  const uint32_t n_cigar = rd16(d + 12);
+  const uint32_t l_seq = rd32(d + 16);
+  const uint64_t tag_off = 32ull + l_read_name + 4ull * n_cigar + (l_seq + 1) / 2 + l_seq;
+  if (tag_off > bs || l_read_name == 0) {
+    e.code = SCT_BAM_EFORMAT;
+    e.msg = "truncated BAM record";
+    return -1;
+  }
+  *qname = (const char*)d + 32;
+  *qlen = l_read_name - 1;  // without the NUL
+  TagVal xf;
+  o.cb = TagVal(), o.ub = TagVal(), o.ge = TagVal();
+  const uint8_t* p = d + tag_off;
+  const uint8_t* end = d + bs;
+  while (p + 3 <= end) {
+    const char a = (char)p[0], b = (char)p[1], t = (char)p[2];
+    p += 3;
+    TagVal v;
+    const size_t used = read_tag(p, end, t, &v);
+    if (!used || p + used > end) {
+      e.code = SCT_BAM_EFORMAT;
+      e.msg = std::string("unsupported or truncated BAM tag type ") + t;
+      return -1;
+    }
+    if (a == tags[0] && b == tags[1]) o.cb = v;
+    if (a == tags[2] && b == tags[3]) o.ub = v;
+    if (a == tags[4] && b == tags[5]) o.ge = v;
+    if (a == 'X' && b == 'F') xf = v;
+    p += used;
+  }
+  uint8_t x = XF_ABSENT;
+  if (xf.present) {
+    x = XF_OTHER;
+    if (xf.is_str && xf.n == 10 && memcmp(xf.s, "INTERGENIC", 10) == 0) x = XF_INTERGENIC;
+  }
+  o.ref = (int32_t)rd32(d), o.pos = (int32_t)rd32(d + 4);
+  o.gq_sum = o.gq_len = o.gq_gt30 = o.cy_gt30 = o.cy_len = o.uy_gt30 = o.uy_len = 0;
+  o.bits = 0, o.xf = x;
+  return 0;
+}
+
 // Per-thread direct-mapped cache in front of the shared tables: cell-sorted input repeats
 // the CB of the previous record and hot genes repeat constantly, so most lookups never take
 // a stripe lock.
@@ -553,10 +605,20 @@ extern "C" {
 const char* sct_bam_last_error(void) { return g_err.c_str(); }
 
 int sct_bam_decode(const char* path, int32_t metric_mode, int32_t n_threads, sct_bam_t** out, int64_t* bad_record) {
+  return sct_bam_decode_tags(path, metric_mode, "CBUBGE", n_threads, out, bad_record);
+}
+
+int sct_bam_decode_tags(const char* path, int32_t metric_mode, const char* tags, int32_t n_threads, sct_bam_t** out,
+                        int64_t* bad_record) {
   g_err.clear();
   if (out) *out = nullptr;
   if (bad_record) *bad_record = -1;
-  if (!path || !out) return fail(SCT_BAM_EIO, "NULL argument");
+  if (!path || !out || !tags) return fail(SCT_BAM_EIO, "NULL argument");
+  if (metric_mode < SCT_BAM_CELL_METRICS || metric_mode > SCT_BAM_COUNT_MATRIX)
+    return fail(SCT_BAM_EIO, "unknown decode mode %d", metric_mode);
+  if (strlen(tags) != 6) return fail(SCT_BAM_EIO, "tags must name three two-character tags");
+  const bool counting = metric_mode == SCT_BAM_COUNT_MATRIX;
+  if (!counting && memcmp(tags, "CBUBGE", 6) != 0) return fail(SCT_BAM_EIO, "the metric modes read CB / UB / GE");
   const bool is_cell = metric_mode == SCT_BAM_CELL_METRICS;
   if (n_threads <= 0) n_threads = omp_get_max_threads();
   const int fd = open(path, O_RDONLY);
@@ -627,6 +689,8 @@ int sct_bam_decode(const char* path, int32_t metric_mode, int32_t n_threads, sct
 
   std::vector<uint64_t> starts;
   int64_t base = 0;
+  std::string prev_qname;  // the last record's query name of the previous window (count mode)
+  bool have_prev = false;
   while (bi < blocks.size() || carry) {
     // 1. inflate the next window of blocks behind the carried bytes
     size_t bj = bi;
@@ -674,6 +738,7 @@ int sct_bam_decode(const char* path, int32_t metric_mode, int32_t n_threads, sct
     // 3. parse + intern
     const int64_t nw = (int64_t)starts.size();
     B->c.resize((size_t)(base + nw));
+    if (counting) B->c.qhead.resize((size_t)(base + nw));
     std::atomic<int64_t> first_bad{INT64_MAX};
     std::mutex err_m;
     RecErr first_err;
@@ -688,7 +753,9 @@ int sct_bam_decode(const char* path, int32_t metric_mode, int32_t n_threads, sct
       for (int64_t i = 0; i < nw; i++) {
         const uint8_t* d = buf.data() + starts[i] + 4;
         const uint32_t bs = rd32(buf.data() + starts[i]);
-        if (parse_record(d, bs, is_cell, o, e)) {
+        const char* qn = nullptr;
+        uint32_t qlen = 0;
+        if (counting ? parse_count_record(d, bs, tags, o, &qn, &qlen, e) : parse_record(d, bs, is_cell, o, e)) {
           std::lock_guard<std::mutex> lk(err_m);
           if (base + i < first_bad.load()) {
             first_bad = base + i;
@@ -697,6 +764,14 @@ int sct_bam_decode(const char* path, int32_t metric_mode, int32_t n_threads, sct
           continue;
         }
         const int64_t j = base + i;
+        if (counting) {
+          // groupby(query_name): a new group where the name differs from the previous record's
+          const uint8_t* pd = i ? buf.data() + starts[i - 1] + 4 : nullptr;
+          bool head;
+          if (pd) head = pd[8] != qlen + 1 || memcmp(pd + 32, qn, qlen) != 0;
+          else head = !have_prev || prev_qname.size() != qlen || memcmp(prev_qname.data(), qn, qlen) != 0;
+          C.qhead[j] = head ? 1 : 0;
+        }
         C.ref[j] = o.ref, C.pos[j] = o.pos;
         C.gq_sum[j] = (uint16_t)o.gq_sum, C.gq_len[j] = (uint16_t)o.gq_len, C.gq_gt30[j] = (uint16_t)o.gq_gt30;
         C.bits[j] = o.bits, C.xf[j] = o.xf;
@@ -715,6 +790,11 @@ int sct_bam_decode(const char* path, int32_t metric_mode, int32_t n_threads, sct
       if (bad_record) *bad_record = first_bad.load();
       return fail(first_err.code, "%s", first_err.msg.c_str());
     }
+    if (counting && nw) {
+      const uint8_t* ld = buf.data() + starts[nw - 1] + 4;
+      prev_qname.assign((const char*)ld + 32, ld[8] ? ld[8] - 1 : 0);
+      have_prev = true;
+    }
     base += nw;
     // 4. carry the cut record
     carry = len - off;
@@ -723,7 +803,7 @@ int sct_bam_decode(const char* path, int32_t metric_mode, int32_t n_threads, sct
     if (bi == blocks.size() && carry == 0) break;
   }
   B->n = base;
-  if (base == 0) return fail(SCT_BAM_EMPTY, "generator raised StopIteration");
+  if (base == 0 && !counting) return fail(SCT_BAM_EMPTY, "generator raised StopIteration");
   // 5. rank the dictionaries: sorted strings, the missing value first
   for (int t = 0; t < 3; t++) {
     std::vector<std::pair<std::string, int32_t>> all;
@@ -770,6 +850,7 @@ const void* sct_bam_column(const sct_bam_t* b, const char* name) {
   if (s == "cy_len") return c.cy_len.data();
   if (s == "uy_gt30") return c.uy_gt30.data();
   if (s == "uy_len") return c.uy_len.data();
+  if (s == "qhead") return c.qhead.empty() && b->n ? nullptr : c.qhead.data();
   return nullptr;
 }
 

@@ -16,6 +16,7 @@
 //   reduce.h    one pass over the globally sorted keys: Counter results from key runs
 //   gene.h      gene buckets -> per-gene partial rows (LDS bins)
 //   finalize.h  partial rows -> output rows; sequential Welford float path
+//   tagsort.h   TagSortBam orders on the device; countmat.h  CountMatrix (CSR)
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared.
 // -ffp-contract=off keeps every Welford operation separately rounded, as Python does.
@@ -24,6 +25,7 @@
 #include <string.h>
 
 #include "common.h"
+#include "countmat.h"
 #include "finalize.h"
 #include "fixedpt.h"
 #include "bucket.h"
@@ -456,6 +458,45 @@ struct SortLayout {
   size_t recs, recs2, ka, kb, va, vb, counts, offsets, sums, bad, total;
 };
 
+struct CountLayout {
+  size_t ka, kb, va, vb, counts, offsets, sums, flags, offs, pair_cell, pair_col, pair_count;
+  size_t cell_first, cell_npairs, cell_pstart, row_of, row_pairs, scalars, total;
+};
+
+CountLayout count_layout(const sct_count_input_t* in) {
+  CountLayout L;
+  const int64_t n1 = in->n > 0 ? in->n : 1;
+  const int64_t c1 = in->n_cell_ids > 0 ? in->n_cell_ids : 1;
+  const int64_t m = n1 > c1 ? n1 : c1;  // the record sort and the cell-order sort share buffers
+  const int64_t cm = (int64_t)kRadix * cdiv(m, kTile);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += align_up(bytes);
+    return o;
+  };
+  L.ka = take(8 * (size_t)m);
+  L.kb = take(8 * (size_t)m);
+  L.va = take(4 * (size_t)m);
+  L.vb = take(4 * (size_t)m);
+  L.counts = take(4 * (size_t)cm);
+  L.offsets = take(4 * (size_t)cm);
+  L.sums = take(8 * (size_t)(cdiv(cm > m ? cm : m, kScanChunk) + 1));
+  L.flags = take(4 * (size_t)n1);
+  L.offs = take(4 * (size_t)n1);
+  L.pair_cell = take(4 * (size_t)n1);
+  L.pair_col = take(4 * (size_t)n1);
+  L.pair_count = take(4 * (size_t)n1);
+  L.cell_first = take(4 * (size_t)c1);
+  L.cell_npairs = take(4 * (size_t)c1);
+  L.cell_pstart = take(4 * (size_t)c1);
+  L.row_of = take(4 * (size_t)c1);
+  L.row_pairs = take(4 * (size_t)c1);
+  L.scalars = take(4 * sizeof(uint64_t));
+  L.total = off;
+  return L;
+}
+
 SortLayout sort_layout(int64_t n) {
   SortLayout L;
   const int64_t n1 = n > 0 ? n : 1;
@@ -753,6 +794,111 @@ int sct_verify_sort(const sct_plan_t* plan, const sct_records_t* rec, const int3
   HIPCHK(hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   *first_violation = h >= none ? -1 : (int64_t)h;
+  return SCT_OK;
+}
+
+int sct_count_matrix_workspace_size(const sct_count_input_t* in, size_t* bytes) {
+  last_error().clear();
+  if (!in || !bytes) return fail(SCT_EINVAL, "NULL argument");
+  *bytes = count_layout(in).total;
+  return SCT_OK;
+}
+
+int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void* workspace, size_t workspace_bytes,
+                     void* stream) {
+  last_error().clear();
+  if (!in || !out) return fail(SCT_EINVAL, "NULL argument");
+  out->n_rows = out->nnz = 0;
+  out->unknown_record = -1;
+  const int64_t n = in->n;
+  if (n < 0 || n >= (int64_t)0x7FFFFFFF) return fail(SCT_EINVAL, "records must be in [0, 2^31 - 1)");
+  if (in->n_cell_ids < 0 || in->n_umi_ids < 0 || in->n_gene_ids < 0 || in->n_cols < 0)
+    return fail(SCT_EINVAL, "negative dictionary size");
+  if (!out->indptr) return fail(SCT_EINVAL, "indptr is NULL");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    HIPCHK(hipMemsetAsync(out->indptr, 0, sizeof(int32_t), s));
+    HIPCHK(hipStreamSynchronize(s));
+    return SCT_OK;
+  }
+  if (!in->cell || !in->umi || !in->gene || !in->xf || !in->qhead || !in->gene_col || !out->row_cell ||
+      !out->indices || !out->data)
+    return fail(SCT_EINVAL, "NULL column");
+  CountKey K;
+  K.cbits = bitlen((uint64_t)in->n_cell_ids);
+  K.colbits = bitlen((uint64_t)(in->n_cols > 0 ? in->n_cols : 1));
+  K.ubits = bitlen((uint64_t)in->n_umi_ids);
+  K.total = K.cbits + K.colbits + K.ubits;
+  if (K.total + 1 > 64)
+    return fail(SCT_EINVAL, "cell (%d) + column (%d) + molecule (%d) id bits exceed 63", K.cbits, K.colbits, K.ubits);
+  const CountLayout L = count_layout(in);
+  if (!workspace || workspace_bytes < L.total)
+    return fail(SCT_ENOMEM, "workspace too small (%zu < %zu)", workspace_bytes, L.total);
+  const int64_t nc = in->n_cell_ids;
+  SortBuffers B{at<uint64_t>(workspace, L.ka), at<uint64_t>(workspace, L.kb), at<uint32_t>(workspace, L.va),
+                at<uint32_t>(workspace, L.vb), at<uint32_t>(workspace, L.counts), at<uint32_t>(workspace, L.offsets),
+                at<uint64_t>(workspace, L.sums)};
+  uint32_t* flags = at<uint32_t>(workspace, L.flags);
+  uint32_t* offs = at<uint32_t>(workspace, L.offs);
+  int32_t* pair_cell = at<int32_t>(workspace, L.pair_cell);
+  int32_t* pair_col = at<int32_t>(workspace, L.pair_col);
+  uint32_t* pair_count = at<uint32_t>(workspace, L.pair_count);
+  uint32_t* cell_first = at<uint32_t>(workspace, L.cell_first);
+  uint32_t* cell_npairs = at<uint32_t>(workspace, L.cell_npairs);
+  uint32_t* cell_pstart = at<uint32_t>(workspace, L.cell_pstart);
+  uint32_t* row_of = at<uint32_t>(workspace, L.row_of);
+  uint32_t* row_pairs = at<uint32_t>(workspace, L.row_pairs);
+  uint64_t* sc = at<uint64_t>(workspace, L.scalars);  // [0] unknown, [1] n_pairs, [2] n_rows, [3] err
+  HIPCHK(hipMemsetAsync(cell_first, 0xFF, sizeof(uint32_t) * (size_t)(nc ? nc : 1), s));
+  HIPCHK(hipMemsetAsync(cell_npairs, 0, sizeof(uint32_t) * (size_t)(nc ? nc : 1), s));
+  HIPCHK(hipMemsetAsync(pair_count, 0, sizeof(uint32_t) * (size_t)n, s));
+  HIPCHK(hipMemsetAsync(sc, 0xFF, sizeof(uint64_t), s));
+  HIPCHK(hipMemsetAsync(sc + 1, 0, 3 * sizeof(uint64_t), s));
+  CountCols c{in->cell, in->umi,     in->gene,       in->xf,         in->qhead,      in->gene_col, n,
+              in->n_cell_ids, in->n_umi_ids, in->n_gene_ids, in->cell_none, in->umi_none, in->n_cols};
+  const dim3 grid((unsigned)cdiv(n, kBlock));
+  LAUNCH("count_groups", k_cm_groups, grid, dim3(kBlock), s, c, K, B.ka, B.va, cell_first,
+         (unsigned long long*)sc, (uint32_t*)(sc + 3));
+  int which = 0;
+  int rc = radix_sort(B, n, K.total + 1, &which, s);
+  if (rc) return rc;
+  const uint64_t* sorted = which ? B.kb : B.ka;
+  LAUNCH("count_pairs", k_cm_pairs, grid, dim3(kBlock), s, sorted, n, K, flags);
+  rc = scan_counts(flags, n, offs, B.sums, s);
+  if (rc) return rc;
+  LAUNCH("count_emit", k_cm_emit, grid, dim3(kBlock), s, sorted, n, K, (const uint32_t*)flags,
+         (const uint32_t*)offs, pair_cell, pair_col, pair_count, cell_pstart, cell_npairs, sc + 1);
+  // row order: counted cells by the record index of their first counted molecule
+  if (nc > 0) {
+    LAUNCH("count_rowkeys", k_cm_rowkeys, dim3((unsigned)cdiv(nc, kBlock)), dim3(kBlock), s,
+           (const uint32_t*)cell_first, (int32_t)nc, B.ka, B.va, sc + 2);
+  }
+  uint64_t h[4];
+  HIPCHK(hipMemcpyAsync(h, sc, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (h[3]) return fail(SCT_EINVAL, "a dictionary id is outside its dictionary");
+  if (h[0] != ~0ull) {
+    out->unknown_record = (int64_t)h[0];
+    return SCT_OK;
+  }
+  const int64_t nnz = (int64_t)h[1], n_rows = (int64_t)h[2];
+  if (n_rows > 0) {
+    rc = radix_sort(B, nc, 32, &which, s);
+    if (rc) return rc;
+    const uint32_t* cells = which ? B.vb : B.va;
+    LAUNCH("count_rows", k_cm_rows, dim3((unsigned)cdiv(n_rows, kBlock)), dim3(kBlock), s, cells, n_rows,
+           (const uint32_t*)cell_npairs, out->row_cell, row_of, row_pairs);
+    rc = scan_counts(row_pairs, n_rows, (uint32_t*)out->indptr, B.sums, s);
+    if (rc) return rc;
+    LAUNCH("count_scatter", k_cm_scatter, dim3((unsigned)cdiv(nnz > 0 ? nnz : 1, kBlock)), dim3(kBlock), s, nnz,
+           (const int32_t*)pair_cell, (const int32_t*)pair_col, (const uint32_t*)pair_count,
+           (const uint32_t*)cell_pstart, (const uint32_t*)row_of, (const int32_t*)out->indptr, out->indices,
+           out->data);
+  }
+  LAUNCH("count_tail", k_cm_set_tail, dim3(1), dim3(kWave), s, out->indptr, n_rows, nnz);
+  HIPCHK(hipStreamSynchronize(s));
+  out->n_rows = n_rows;
+  out->nnz = nnz;
   return SCT_OK;
 }
 

@@ -220,6 +220,43 @@ class Engine:
                                          self._stream()))
         return int(out.value)
 
+    # ---- count matrix (CountMatrix.from_sorted_tagged_bam, count.py:134-328) ----
+    def count_matrix(self, cell: torch.Tensor, umi: torch.Tensor, gene: torch.Tensor, xf: torch.Tensor,
+                     qhead: torch.Tensor, gene_col: torch.Tensor, n_cell_ids: int, n_umi_ids: int, cell_none: int,
+                     umi_none: int, n_cols: int):
+        """CSR of the molecule counts: (row_cell, indptr, indices, data) device tensors and the first
+        record index of a counted molecule whose gene is outside the annotation (-1 if none; the
+        matrix is then not built).  Columns are int32 ids / uint8 codes on this engine's device."""
+        n = int(cell.numel())
+        for t in (umi, gene, xf, qhead):
+            if int(t.numel()) != n:
+                raise ValueError("record columns differ in length")
+        ci = N.CountInput()
+        ci.n = n
+        ci.cell, ci.umi, ci.gene = cell.data_ptr(), umi.data_ptr(), gene.data_ptr()
+        ci.xf, ci.qhead = xf.data_ptr(), qhead.data_ptr()
+        ci.n_cell_ids, ci.n_umi_ids, ci.n_gene_ids = int(n_cell_ids), int(n_umi_ids), int(gene_col.numel())
+        ci.cell_none, ci.umi_none = int(cell_none), int(umi_none)
+        ci.gene_col, ci.n_cols = gene_col.data_ptr(), int(n_cols)
+        nbytes = ctypes.c_size_t(0)
+        N.check(self.lib.sct_count_matrix_workspace_size(ctypes.byref(ci), ctypes.byref(nbytes)))
+        ws = torch.empty(int(nbytes.value), dtype=torch.uint8, device=self.device)
+        nc = max(1, int(n_cell_ids))
+        row_cell = torch.empty(nc, dtype=torch.int32, device=self.device)
+        indptr = torch.empty(nc + 1, dtype=torch.int32, device=self.device)
+        indices = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+        data = torch.empty(max(1, n), dtype=torch.int32, device=self.device)  # uint32 counts (< 2^31)
+        co = N.CountOutput()
+        co.row_cell, co.indptr, co.indices, co.data = (row_cell.data_ptr(), indptr.data_ptr(), indices.data_ptr(),
+                                                       data.data_ptr())
+        N.check(self.lib.sct_count_matrix(ctypes.byref(ci), ctypes.byref(co), ctypes.c_void_p(ws.data_ptr()),
+                                          ws.numel(), self._stream()))
+        del ws
+        if co.unknown_record >= 0:
+            return None, int(co.unknown_record)
+        r, z = int(co.n_rows), int(co.nnz)
+        return (row_cell[:r], indptr[:r + 1], indices[:z], data[:z]), -1
+
     # ---- profiling (HIP events inside the library) ----
     def profile_enable(self, on: bool = True):
         self.lib.sct_profile_enable(1 if on else 0)

@@ -8,6 +8,8 @@ codes as the reference's ``GenericPlatform`` metric commands
   CalculateGeneMetrics -i BAM -o STEM
   MergeCellMetrics FILES... -o STEM
   MergeGeneMetrics FILES... -o STEM
+  CreateCountMatrix -b BAM -o PREFIX -a GTF [-c TAG -m TAG -g TAG -n]   (platform.py:384-470)
+  MergeCountMatrices -i PREFIX... -o STEM                              (platform.py:475-516)
 
 New flags are optional only: ``--float-mode {welford,exact}`` and ``--device``.
 Run as ``python -m sctools_amd <Command> [args]``.
@@ -16,7 +18,7 @@ Run as ``python -m sctools_amd <Command> [args]``.
 import argparse
 from typing import Iterable, Set
 
-from sctools_amd import gtf, metrics
+from sctools_amd import consts, count, gtf, metrics
 
 
 def _engine_args(parser):
@@ -74,6 +76,50 @@ class GenericPlatform:
         return 0
 
 
+    @classmethod
+    def bam_to_count_matrix(cls, args: Iterable[str] = None) -> int:
+        """CreateCountMatrix (platform.py:384-470): query-name-grouped tagged BAM -> CSR count matrix."""
+        parser = argparse.ArgumentParser()
+        parser.set_defaults(cell_barcode_tag=consts.CELL_BARCODE_TAG_KEY,
+                            molecule_barcode_tag=consts.MOLECULE_BARCODE_TAG_KEY,
+                            gene_name_tag=consts.GENE_NAME_TAG_KEY, sn_rna_seq_mode=False)
+        parser.add_argument("-b", "--bam-file", help="input_bam_file", required=True)
+        parser.add_argument("-o", "--output-prefix", help="file stem for count matrix", required=True)
+        parser.add_argument("-a", "--gtf-annotation-file", required=True,
+                            help="gtf annotation file that bam_file was aligned against")
+        parser.add_argument("-c", "--cell-barcode-tag",
+                            help="tag that identifies the cell barcode (default = %s)" % consts.CELL_BARCODE_TAG_KEY)
+        parser.add_argument("-m", "--molecule-barcode-tag", help="tag that identifies the molecule barcode "
+                            "(default = %s)" % consts.MOLECULE_BARCODE_TAG_KEY)
+        parser.add_argument("-g", "--gene-id-tag",
+                            help="tag that identifies the gene name (default = %s)" % consts.GENE_NAME_TAG_KEY)
+        parser.add_argument("-n", "--sn-rna-seq-mode", action="store_true", help="snRNA Seq mode (default = False)")
+        parser.add_argument("--device", default=None, help="torch device (default: current GPU)")
+        args = parser.parse_args(args) if args is not None else parser.parse_args()
+        open_mode = "r" if args.bam_file.endswith(".sam") else "rb"
+        gene_name_to_index = gtf.extract_gene_names(args.gtf_annotation_file)
+        gene_locations = gtf.extract_extended_gene_names(args.gtf_annotation_file) if args.sn_rna_seq_mode else None
+        matrix = count.CountMatrix.from_sorted_tagged_bam(
+            bam_file=args.bam_file, gene_name_to_index=gene_name_to_index,
+            chromosomes_gene_locations_extended=gene_locations, cell_barcode_tag=args.cell_barcode_tag,
+            molecule_barcode_tag=args.molecule_barcode_tag, gene_name_tag=args.gene_id_tag, open_mode=open_mode,
+            device=args.device)
+        matrix.save(args.output_prefix)
+        return 0
+
+    @classmethod
+    def merge_count_matrices(cls, args: Iterable[str] = None) -> int:
+        """MergeCountMatrices (platform.py:475-516)."""
+        parser = argparse.ArgumentParser()
+        parser.add_argument("-i", "--input-prefixes", nargs="+", help="prefix for count matrices to be concatenated. "
+                            "e.g. test_counts for test_counts.npz, test_counts_col_index.npy, and "
+                            "test_counts_row_index.npy")
+        parser.add_argument("-o", "--output-stem", help="file stem for merged csr matrix", required=True)
+        args = parser.parse_args(args) if args is not None else parser.parse_args()
+        count.CountMatrix.merge_matrices(args.input_prefixes).save(args.output_stem)
+        return 0
+
+
 class TenXV2(GenericPlatform):
     """The reference exposes the metric commands on TenXV2 too (platform.py:579)."""
 
@@ -83,4 +129,6 @@ COMMANDS = {
     "CalculateGeneMetrics": GenericPlatform.calculate_gene_metrics,
     "MergeCellMetrics": GenericPlatform.merge_cell_metrics,
     "MergeGeneMetrics": GenericPlatform.merge_gene_metrics,
+    "CreateCountMatrix": GenericPlatform.bam_to_count_matrix,
+    "MergeCountMatrices": GenericPlatform.merge_count_matrices,
 }
