@@ -6,19 +6,22 @@
 // CSR conversion then sums the entries of each (cell, gene).  That is order-free except for
 // the row order (a cell's row is numbered when its first molecule is counted), so:
 //
-//   k_cm_groups   one lane per query-name group head: the group's molecule key
-//                 [cell | column | umi] or a "dropped" top bit; atomicMin of the group's
-//                 record index per cell (row order) and over unknown genes (the KeyError)
-//   radix.h       LSD sort of the keys (cbits + colbits + ubits + 1 bits)
-//   k_cm_pairs    triple heads / (cell, column) pair heads in the sorted keys
-//   scan.h        exclusive scan of the pair-head flags -> pair index
-//   k_cm_emit     per pair: cell, column, molecule count (triples of the pair)
-//   k_cm_rowkeys  (first record index, cell) per counted cell -> radix.h -> row order
-//   k_cm_rows     row -> cell, cell -> row, pairs per row; scan -> CSR indptr
-//   k_cm_scatter  pairs (cell-id order) -> CSR rows (first-molecule order)
+//   k_cm_groups    one lane per query-name group head: the group's molecule key
+//                  [cell | column | umi] and a keep flag; a wave-aggregated atomicMin of
+//                  the group's record index per cell (row order) and over unknown genes
+//   scan + k_cm_compact   kept keys -> a dense array (about half the records)
+//   radix.h        LSD sort of the kept keys (cbits + colbits + ubits bits)
+//   k_cm_heads     triple-head and (cell, column) pair-head flags; two scans number them
+//   k_cm_emit      per pair: cell, column, index of its first triple, first pair of a cell
+//   k_cm_cells     pairs per cell (from the cell's last pair)
+//   k_cm_rowkeys   (first record index, cell) per counted cell -> radix.h -> row order
+//   k_cm_rows      row -> cell, cell -> row, pairs per row; scan -> CSR indptr
+//   k_cm_scatter   pairs (cell-id order) -> CSR rows (first-molecule order); the count of a
+//                  pair = triples between its first triple and the next pair's
 //
-// HBM-bound integer work: ~14 bytes read per record in k_cm_groups, 12 bytes written, then
-// the radix passes over 12-byte (key, value) items.
+// No global atomics on the hot arrays: counts come from scans, so cell-sorted input (every
+// lane of a wave on the same cell) costs the same as shuffled input.  HBM-bound integer
+// work; see DESIGN.md §10 for the bytes per record of each kernel.
 #pragma once
 #include "radix.h"
 #include "scan.h"
@@ -27,7 +30,7 @@
 namespace sct {
 
 struct CountKey {
-  int cbits, colbits, ubits, total;  // total = cbits + colbits + ubits; bit `total` = dropped
+  int cbits, colbits, ubits, total;  // total = cbits + colbits + ubits
 };
 
 struct CountCols {
@@ -40,19 +43,48 @@ struct CountCols {
 
 constexpr uint8_t kXfAbsent = 0, kXfIntergenic = 4;  // SCT_XF_ABSENT / SCT_XF_INTERGENIC
 
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const T o = __shfl_xor(v, off);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// atomicMin(&dst[slot], v) for the lanes with `on`, combined across lanes with equal slots:
+// a few leader rounds (cell-grouped input puts one or two cells in a wave), then per lane.
+// Call from every lane of the wave.
+__device__ __forceinline__ void wave_atomic_min(uint32_t* dst, bool on, uint32_t slot, uint32_t v) {
+  const int lane = threadIdx.x & (kWave - 1);
+  bool mine = on;
+  for (int round = 0; round < 4; round++) {
+    const uint64_t active = __ballot(mine);
+    if (!active) return;
+    const int leader = __ffsll((unsigned long long)active) - 1;
+    const uint32_t s = __shfl(slot, leader);
+    const bool take = mine && slot == s;
+    const uint32_t m = wave_min(take ? v : 0xFFFFFFFFu);
+    if (lane == leader) atomicMin(&dst[s], m);
+    if (take) mine = false;
+  }
+  if (mine) atomicMin(&dst[slot], v);
+}
+
 // count.py:222-270 for the group starting at record i (qhead[i] == 1): cell / molecule of its
-// first record; the implicated gene names are the single-name GE values of alignments with
-// an XF tag other than INTERGENIC (gene_col != SKIP covers "has GE" and "no ','"); the group
-// counts when exactly one distinct name is implicated -- for a one-alignment group that is
-// the same test.
-__global__ void k_cm_groups(CountCols c, CountKey K, uint64_t* __restrict__ keys, uint32_t* __restrict__ vals,
+// first record; the implicated gene names are the single-name gene values of alignments with
+// an XF tag other than INTERGENIC (gene_col != SKIP covers "has the tag" and "no ','"); the
+// group counts when exactly one distinct name is implicated -- for a one-alignment group that
+// is the same test.
+__global__ void k_cm_groups(CountCols c, CountKey K, uint64_t* __restrict__ keys, uint32_t* __restrict__ keep,
                             uint32_t* __restrict__ cell_first, unsigned long long* __restrict__ unknown,
                             uint32_t* __restrict__ err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= c.n) return;
-  uint64_t key = 1ull << K.total;
-  if (c.qhead[i] || i == 0) {
-    const int32_t cell = c.cell[i], umi = c.umi[i];
+  bool kept = false;
+  int32_t cell = 0;
+  if (i < c.n && (c.qhead[i] || i == 0)) {
+    cell = c.cell[i];
+    const int32_t umi = c.umi[i];
     if ((uint32_t)cell >= (uint32_t)c.n_cell || (uint32_t)umi >= (uint32_t)c.n_umi) {
       atomicOr(err, 1u);
     } else if (cell != c.cell_none && umi != c.umi_none) {
@@ -76,57 +108,64 @@ __global__ void k_cm_groups(CountCols c, CountKey K, uint64_t* __restrict__ keys
           atomicMin(unknown, (unsigned long long)i);
           col = 0;
         }
-        key = ((uint64_t)cell << (K.colbits + K.ubits)) | ((uint64_t)col << K.ubits) | (uint64_t)umi;
-        atomicMin(&cell_first[cell], (uint32_t)i);
+        keys[i] = ((uint64_t)cell << (K.colbits + K.ubits)) | ((uint64_t)col << K.ubits) | (uint64_t)umi;
+        kept = true;
       }
     }
   }
-  keys[i] = key;
-  vals[i] = (uint32_t)i;
+  if (i < c.n) keep[i] = kept ? 1u : 0u;
+  wave_atomic_min(cell_first, kept, (uint32_t)cell, (uint32_t)i);
 }
 
-struct CmHead {
-  bool triple, pair, first_of_cell;
-};
-
-__device__ inline CmHead cm_head(const uint64_t* keys, int64_t i, CountKey K) {
-  const uint64_t k = keys[i];
-  CmHead h{false, false, false};
-  if (k >> K.total) return h;  // dropped (sorted last)
-  if (i == 0) return CmHead{true, true, true};
-  const uint64_t p = keys[i - 1];  // valid: dropped keys sort after every valid one
-  h.triple = p != k;
-  h.pair = h.triple && (p >> K.ubits) != (k >> K.ubits);
-  h.first_of_cell = h.pair && (p >> (K.ubits + K.colbits)) != (k >> (K.ubits + K.colbits));
-  return h;
-}
-
-__global__ void k_cm_pairs(const uint64_t* __restrict__ keys, int64_t n, CountKey K, uint32_t* __restrict__ flags) {
+__global__ void k_cm_compact(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ keep,
+                             const uint32_t* __restrict__ offs, int64_t n, uint64_t* __restrict__ out,
+                             uint32_t* __restrict__ out_vals, uint64_t* __restrict__ n_kept) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  flags[i] = cm_head(keys, i, K).pair ? 1u : 0u;
+  if (i == n - 1) *n_kept = (uint64_t)offs[i] + keep[i];
+  if (!keep[i]) return;
+  out[offs[i]] = keys[i];
+  out_vals[offs[i]] = (uint32_t)i;
 }
 
-// pair index of a triple head = (pair heads before it, inclusive) - 1
-__global__ void k_cm_emit(const uint64_t* __restrict__ keys, int64_t n, CountKey K, const uint32_t* __restrict__ flags,
-                          const uint32_t* __restrict__ offs, int32_t* __restrict__ pair_cell,
-                          int32_t* __restrict__ pair_col, uint32_t* __restrict__ pair_count,
-                          uint32_t* __restrict__ cell_pstart, uint32_t* __restrict__ cell_npairs,
-                          uint64_t* __restrict__ n_pairs) {
+__global__ void k_cm_heads(const uint64_t* __restrict__ keys, int64_t m, CountKey K, uint32_t* __restrict__ triple,
+                           uint32_t* __restrict__ pair) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (i == n - 1) *n_pairs = (uint64_t)offs[i] + flags[i];
-  const CmHead h = cm_head(keys, i, K);
-  if (!h.triple) return;
+  if (i >= m) return;
   const uint64_t k = keys[i];
-  const uint32_t p = offs[i] + (h.pair ? 0u : 0xFFFFFFFFu);
-  atomicAdd(&pair_count[p], 1u);
-  if (!h.pair) return;
-  const int32_t cell = (int32_t)(k >> (K.ubits + K.colbits));
+  const uint64_t p = i ? keys[i - 1] : ~k;
+  triple[i] = p != k ? 1u : 0u;
+  pair[i] = (p >> K.ubits) != (k >> K.ubits) ? 1u : 0u;
+}
+
+__global__ void k_cm_emit(const uint64_t* __restrict__ keys, int64_t m, CountKey K, const uint32_t* __restrict__ pair,
+                          const uint32_t* __restrict__ pair_off, const uint32_t* __restrict__ triple,
+                          const uint32_t* __restrict__ triple_off, int32_t* __restrict__ pair_cell,
+                          int32_t* __restrict__ pair_col, uint32_t* __restrict__ pair_tri,
+                          uint32_t* __restrict__ cell_pstart, uint64_t* __restrict__ totals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  if (i == m - 1) {
+    totals[0] = (uint64_t)pair_off[i] + pair[i];
+    totals[1] = (uint64_t)triple_off[i] + triple[i];
+  }
+  if (!pair[i]) return;
+  const uint64_t k = keys[i];
+  const uint32_t p = pair_off[i];
+  const int cs = K.ubits + K.colbits;
+  const int32_t cell = (int32_t)(k >> cs);
   pair_cell[p] = cell;
   pair_col[p] = (int32_t)((k >> K.ubits) & ((1ull << K.colbits) - 1));
-  atomicAdd(&cell_npairs[cell], 1u);
-  if (h.first_of_cell) cell_pstart[cell] = p;
+  pair_tri[p] = triple_off[i];
+  if (i == 0 || (keys[i - 1] >> cs) != (k >> cs)) cell_pstart[cell] = p;
+}
+
+__global__ void k_cm_cells(const int32_t* __restrict__ pair_cell, int64_t nnz, const uint32_t* __restrict__ cell_pstart,
+                           uint32_t* __restrict__ cell_npairs) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nnz) return;
+  const int32_t c = pair_cell[p];
+  if (p == nnz - 1 || pair_cell[p + 1] != c) cell_npairs[c] = (uint32_t)(p + 1 - cell_pstart[c]);
 }
 
 __global__ void k_cm_rowkeys(const uint32_t* __restrict__ cell_first, int32_t n_cell, uint64_t* __restrict__ keys,
@@ -151,16 +190,18 @@ __global__ void k_cm_rows(const uint32_t* __restrict__ sorted_cells, int64_t n_r
   row_pairs[r] = cell_npairs[c];
 }
 
-__global__ void k_cm_scatter(int64_t nnz, const int32_t* __restrict__ pair_cell, const int32_t* __restrict__ pair_col,
-                             const uint32_t* __restrict__ pair_count, const uint32_t* __restrict__ cell_pstart,
-                             const uint32_t* __restrict__ row_of, const int32_t* __restrict__ indptr,
-                             int32_t* __restrict__ indices, uint32_t* __restrict__ data) {
+__global__ void k_cm_scatter(int64_t nnz, uint64_t n_triples, const int32_t* __restrict__ pair_cell,
+                             const int32_t* __restrict__ pair_col, const uint32_t* __restrict__ pair_tri,
+                             const uint32_t* __restrict__ cell_pstart, const uint32_t* __restrict__ row_of,
+                             const int32_t* __restrict__ indptr, int32_t* __restrict__ indices,
+                             uint32_t* __restrict__ data) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= nnz) return;
   const int32_t c = pair_cell[p];
   const int64_t dst = (int64_t)indptr[row_of[c]] + (p - (int64_t)cell_pstart[c]);
+  const uint64_t next = p + 1 < nnz ? (uint64_t)pair_tri[p + 1] : n_triples;
   indices[dst] = pair_col[p];
-  data[dst] = pair_count[p];
+  data[dst] = (uint32_t)(next - pair_tri[p]);
 }
 
 __global__ void k_cm_set_tail(int32_t* __restrict__ indptr, int64_t n_rows, int64_t nnz) {

@@ -459,7 +459,7 @@ struct SortLayout {
 };
 
 struct CountLayout {
-  size_t ka, kb, va, vb, counts, offsets, sums, flags, offs, pair_cell, pair_col, pair_count;
+  size_t ka, kb, va, vb, counts, offsets, sums, flags_a, offs_a, flags_b, offs_b, pair_cell, pair_col, pair_tri;
   size_t cell_first, cell_npairs, cell_pstart, row_of, row_pairs, scalars, total;
 };
 
@@ -482,17 +482,19 @@ CountLayout count_layout(const sct_count_input_t* in) {
   L.counts = take(4 * (size_t)cm);
   L.offsets = take(4 * (size_t)cm);
   L.sums = take(8 * (size_t)(cdiv(cm > m ? cm : m, kScanChunk) + 1));
-  L.flags = take(4 * (size_t)n1);
-  L.offs = take(4 * (size_t)n1);
+  L.flags_a = take(4 * (size_t)n1);
+  L.offs_a = take(4 * (size_t)n1);
+  L.flags_b = take(4 * (size_t)n1);
+  L.offs_b = take(4 * (size_t)n1);
   L.pair_cell = take(4 * (size_t)n1);
   L.pair_col = take(4 * (size_t)n1);
-  L.pair_count = take(4 * (size_t)n1);
+  L.pair_tri = take(4 * (size_t)n1);
   L.cell_first = take(4 * (size_t)c1);
   L.cell_npairs = take(4 * (size_t)c1);
   L.cell_pstart = take(4 * (size_t)c1);
   L.row_of = take(4 * (size_t)c1);
   L.row_pairs = take(4 * (size_t)c1);
-  L.scalars = take(4 * sizeof(uint64_t));
+  L.scalars = take(6 * sizeof(uint64_t));
   L.total = off;
   return L;
 }
@@ -829,7 +831,7 @@ int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void*
   K.colbits = bitlen((uint64_t)(in->n_cols > 0 ? in->n_cols : 1));
   K.ubits = bitlen((uint64_t)in->n_umi_ids);
   K.total = K.cbits + K.colbits + K.ubits;
-  if (K.total + 1 > 64)
+  if (K.total > 63)
     return fail(SCT_EINVAL, "cell (%d) + column (%d) + molecule (%d) id bits exceed 63", K.cbits, K.colbits, K.ubits);
   const CountLayout L = count_layout(in);
   if (!workspace || workspace_bytes < L.total)
@@ -838,51 +840,67 @@ int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void*
   SortBuffers B{at<uint64_t>(workspace, L.ka), at<uint64_t>(workspace, L.kb), at<uint32_t>(workspace, L.va),
                 at<uint32_t>(workspace, L.vb), at<uint32_t>(workspace, L.counts), at<uint32_t>(workspace, L.offsets),
                 at<uint64_t>(workspace, L.sums)};
-  uint32_t* flags = at<uint32_t>(workspace, L.flags);
-  uint32_t* offs = at<uint32_t>(workspace, L.offs);
+  uint32_t* fa = at<uint32_t>(workspace, L.flags_a);
+  uint32_t* oa = at<uint32_t>(workspace, L.offs_a);
+  uint32_t* fb = at<uint32_t>(workspace, L.flags_b);
+  uint32_t* ob = at<uint32_t>(workspace, L.offs_b);
   int32_t* pair_cell = at<int32_t>(workspace, L.pair_cell);
   int32_t* pair_col = at<int32_t>(workspace, L.pair_col);
-  uint32_t* pair_count = at<uint32_t>(workspace, L.pair_count);
+  uint32_t* pair_tri = at<uint32_t>(workspace, L.pair_tri);
   uint32_t* cell_first = at<uint32_t>(workspace, L.cell_first);
   uint32_t* cell_npairs = at<uint32_t>(workspace, L.cell_npairs);
   uint32_t* cell_pstart = at<uint32_t>(workspace, L.cell_pstart);
   uint32_t* row_of = at<uint32_t>(workspace, L.row_of);
   uint32_t* row_pairs = at<uint32_t>(workspace, L.row_pairs);
-  uint64_t* sc = at<uint64_t>(workspace, L.scalars);  // [0] unknown, [1] n_pairs, [2] n_rows, [3] err
+  // scalars: [0] unknown record, [1] kept groups, [2] pairs, [3] triples, [4] rows, [5] err
+  uint64_t* sc = at<uint64_t>(workspace, L.scalars);
   HIPCHK(hipMemsetAsync(cell_first, 0xFF, sizeof(uint32_t) * (size_t)(nc ? nc : 1), s));
-  HIPCHK(hipMemsetAsync(cell_npairs, 0, sizeof(uint32_t) * (size_t)(nc ? nc : 1), s));
-  HIPCHK(hipMemsetAsync(pair_count, 0, sizeof(uint32_t) * (size_t)n, s));
   HIPCHK(hipMemsetAsync(sc, 0xFF, sizeof(uint64_t), s));
-  HIPCHK(hipMemsetAsync(sc + 1, 0, 3 * sizeof(uint64_t), s));
+  HIPCHK(hipMemsetAsync(sc + 1, 0, 5 * sizeof(uint64_t), s));
   CountCols c{in->cell, in->umi,     in->gene,       in->xf,         in->qhead,      in->gene_col, n,
               in->n_cell_ids, in->n_umi_ids, in->n_gene_ids, in->cell_none, in->umi_none, in->n_cols};
-  const dim3 grid((unsigned)cdiv(n, kBlock));
-  LAUNCH("count_groups", k_cm_groups, grid, dim3(kBlock), s, c, K, B.ka, B.va, cell_first,
-         (unsigned long long*)sc, (uint32_t*)(sc + 3));
-  int which = 0;
-  int rc = radix_sort(B, n, K.total + 1, &which, s);
+  // 1. molecule keys of the counted groups, compacted
+  LAUNCH("count_groups", k_cm_groups, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), s, c, K, B.kb, fa, cell_first,
+         (unsigned long long*)sc, (uint32_t*)(sc + 5));
+  int rc = scan_counts(fa, n, oa, B.sums, s);
   if (rc) return rc;
-  const uint64_t* sorted = which ? B.kb : B.ka;
-  LAUNCH("count_pairs", k_cm_pairs, grid, dim3(kBlock), s, sorted, n, K, flags);
-  rc = scan_counts(flags, n, offs, B.sums, s);
-  if (rc) return rc;
-  LAUNCH("count_emit", k_cm_emit, grid, dim3(kBlock), s, sorted, n, K, (const uint32_t*)flags,
-         (const uint32_t*)offs, pair_cell, pair_col, pair_count, cell_pstart, cell_npairs, sc + 1);
-  // row order: counted cells by the record index of their first counted molecule
-  if (nc > 0) {
-    LAUNCH("count_rowkeys", k_cm_rowkeys, dim3((unsigned)cdiv(nc, kBlock)), dim3(kBlock), s,
-           (const uint32_t*)cell_first, (int32_t)nc, B.ka, B.va, sc + 2);
-  }
-  uint64_t h[4];
+  LAUNCH("count_compact", k_cm_compact, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), s, (const uint64_t*)B.kb,
+         (const uint32_t*)fa, (const uint32_t*)oa, n, B.ka, B.va, sc + 1);
+  uint64_t h[6];
   HIPCHK(hipMemcpyAsync(h, sc, sizeof(h), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  if (h[3]) return fail(SCT_EINVAL, "a dictionary id is outside its dictionary");
+  if (h[5]) return fail(SCT_EINVAL, "a dictionary id is outside its dictionary");
   if (h[0] != ~0ull) {
     out->unknown_record = (int64_t)h[0];
     return SCT_OK;
   }
-  const int64_t nnz = (int64_t)h[1], n_rows = (int64_t)h[2];
-  if (n_rows > 0) {
+  const int64_t m = (int64_t)h[1];
+  int64_t nnz = 0, n_rows = 0;
+  uint64_t n_triples = 0;
+  if (m > 0) {
+    // 2. sort; triples and (cell, column) pairs numbered by scans
+    int which = 0;
+    rc = radix_sort(B, m, K.total, &which, s);
+    if (rc) return rc;
+    const uint64_t* sorted = which ? B.kb : B.ka;
+    const dim3 grid((unsigned)cdiv(m, kBlock));
+    LAUNCH("count_heads", k_cm_heads, grid, dim3(kBlock), s, sorted, m, K, fa, fb);
+    rc = scan_counts(fa, m, oa, B.sums, s);
+    if (rc) return rc;
+    rc = scan_counts(fb, m, ob, B.sums, s);
+    if (rc) return rc;
+    LAUNCH("count_emit", k_cm_emit, grid, dim3(kBlock), s, sorted, m, K, (const uint32_t*)fb, (const uint32_t*)ob,
+           (const uint32_t*)fa, (const uint32_t*)oa, pair_cell, pair_col, pair_tri, cell_pstart, sc + 2);
+    // 3. row order: counted cells by the record index of their first counted molecule
+    LAUNCH("count_rowkeys", k_cm_rowkeys, dim3((unsigned)cdiv(nc, kBlock)), dim3(kBlock), s,
+           (const uint32_t*)cell_first, (int32_t)nc, B.ka, B.va, sc + 4);
+    HIPCHK(hipMemcpyAsync(h, sc, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    nnz = (int64_t)h[2];
+    n_triples = h[3];
+    n_rows = (int64_t)h[4];
+    LAUNCH("count_cells", k_cm_cells, dim3((unsigned)cdiv(nnz, kBlock)), dim3(kBlock), s, (const int32_t*)pair_cell,
+           nnz, (const uint32_t*)cell_pstart, cell_npairs);
     rc = radix_sort(B, nc, 32, &which, s);
     if (rc) return rc;
     const uint32_t* cells = which ? B.vb : B.va;
@@ -890,8 +908,8 @@ int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void*
            (const uint32_t*)cell_npairs, out->row_cell, row_of, row_pairs);
     rc = scan_counts(row_pairs, n_rows, (uint32_t*)out->indptr, B.sums, s);
     if (rc) return rc;
-    LAUNCH("count_scatter", k_cm_scatter, dim3((unsigned)cdiv(nnz > 0 ? nnz : 1, kBlock)), dim3(kBlock), s, nnz,
-           (const int32_t*)pair_cell, (const int32_t*)pair_col, (const uint32_t*)pair_count,
+    LAUNCH("count_scatter", k_cm_scatter, dim3((unsigned)cdiv(nnz, kBlock)), dim3(kBlock), s, nnz, n_triples,
+           (const int32_t*)pair_cell, (const int32_t*)pair_col, (const uint32_t*)pair_tri,
            (const uint32_t*)cell_pstart, (const uint32_t*)row_of, (const int32_t*)out->indptr, out->indices,
            out->data);
   }
