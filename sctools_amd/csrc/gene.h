@@ -197,12 +197,55 @@ struct GeneAcc {
   }
 };
 
+// Segmented inclusive DPP scan of one value over the wave: lanes hold partial sums of the
+// segment (contiguous lanes with equal keys) that starts at lane `seg`; m[0..5] say whether
+// the source lane of each step (row_shr 1, 2, 4, 8; row_bcast 15; row_bcast 31) lies inside
+// the lane's segment.  Afterwards the last lane of every segment holds the segment's sum.
+template <typename T>
+__device__ __forceinline__ T seg_scan_dpp(T v, const bool (&m)[6]) {
+  T x;
+  x = dpp_val<0x111, 0xf>(v);  // row_shr:1
+  v += m[0] ? x : (T)0;
+  x = dpp_val<0x112, 0xf>(v);  // row_shr:2
+  v += m[1] ? x : (T)0;
+  x = dpp_val<0x114, 0xf>(v);  // row_shr:4
+  v += m[2] ? x : (T)0;
+  x = dpp_val<0x118, 0xf>(v);  // row_shr:8
+  v += m[3] ? x : (T)0;
+  x = dpp_val<0x142, 0xa>(v);  // row_bcast:15 (rows 1, 3 get lanes 15, 47)
+  v += m[4] ? x : (T)0;
+  x = dpp_val<0x143, 0xc>(v);  // row_bcast:31 (rows 2, 3 get lane 31)
+  v += m[5] ? x : (T)0;
+  return v;
+}
+
+// Flush the wave's run accumulators: lanes hold runs of gene `key` (-1: none), equal keys in
+// contiguous lanes (the sub-tile is sorted and every thread owns consecutive payloads).  One
+// segmented scan per lane value, then the last lane of each segment adds its gene's sums to
+// the LDS bins -- one atomic per (segment, value) and no two lanes on one address, instead of
+// every lane adding its own run (up to 64 lanes on one bin).  Every lane must call it, all
+// active.
+__device__ __forceinline__ void gene_wave_flush(GeneAcc& acc, int key, int32_t* s_cbin, unsigned long long* s_lbin) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int prev = __shfl_up(key, 1);
+  const uint64_t heads = __ballot(lane == 0 || prev != key);
+  const uint64_t upto = lane == kWave - 1 ? ~0ull : ((1ull << (lane + 1)) - 1);
+  const int seg = kWave - 1 - __clzll((unsigned long long)(heads & upto));
+  const bool m[6] = {seg <= lane - 1, seg <= lane - 2, seg <= lane - 4, seg <= lane - 8, seg < (lane & ~15), seg <= 31};
+#pragma unroll
+  for (int i = 0; i < kGeneCnt; i++) acc.c[i] = seg_scan_dpp(acc.c[i], m);
+#pragma unroll
+  for (int i = 0; i < 3 * kStreamLanes; i++) acc.l[i] = seg_scan_dpp(acc.l[i], m);
+  const bool tail = lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull);
+  if (tail && key >= 0) acc.flush(&s_cbin[key * kGeneCntPad], &s_lbin[key * 3 * kStreamLanes]);
+}
+
 // One work item = (gene bucket, range of its payloads).  Each sub-tile of kGeneSub payloads is
 // counting-sorted in LDS by local gene id, so every thread's kGeneItems consecutive payloads are
-// long runs of one gene: registers accumulate a run and flush it into the LDS bins once.  The
-// run survives sub-tiles: sorted sub-tiles of one bucket put the same genes at similar
-// positions, so a thread keeps adding to one gene and flushes on change.  (The flushes -- 39
-// LDS atomics per finished run -- are most of the kernel's time; see DESIGN.md.)
+// long runs of one gene: registers accumulate a run; a run that ends inside the thread's
+// payloads goes to the LDS bins directly, and the runs still open at the end of the sub-tile
+// are combined across the wave by a segmented DPP scan (gene_wave_flush), so one lane per
+// gene per wave adds the 39 lanes (15 counters, 24 exact-sum lanes) to the bins.
 __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __restrict__ pay,
                                                         const int64_t* __restrict__ work,
                                                         const int64_t* __restrict__ n_work, int32_t n_gene_ids,
@@ -267,16 +310,19 @@ __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __res
       const uint4 w = s_sorted[j0 + k];
       const GenePayload& g = *reinterpret_cast<const GenePayload*>(&w);
       const int lg = (int)(g.gene - g0);
-      if (lg != cur) {
+      if (lg != cur) {  // a gene boundary inside the thread's payloads: its own bin, no conflict
         if (cur >= 0) acc.flush(&s_cbin[cur * kGeneCntPad], &s_lbin[cur * 3 * kStreamLanes]);
         acc.clear();
         cur = lg;
       }
       acc.add(g, s_rcp);
     }
+    // the thread's last run joins its neighbours' runs of the same gene
+    gene_wave_flush(acc, cur, s_cbin, s_lbin);
+    acc.clear();
+    cur = -1;
     __syncthreads();  // s_sorted / s_cnt are reused by the next sub-tile
   }
-  if (cur >= 0) acc.flush(&s_cbin[cur * kGeneCntPad], &s_lbin[cur * 3 * kStreamLanes]);
   __syncthreads();
   // bins -> partial rows: counter lanes 0..14 are partial slots 0..14; stream lanes follow P_FLOAT
   for (int i = t; i < kGenesPerBucket * kGeneCnt; i += kBlock) {

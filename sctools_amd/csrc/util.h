@@ -269,6 +269,11 @@ __device__ __forceinline__ int64_t dpp_i64(int64_t v) {
   const uint32_t hi = (uint32_t)dpp_i32<kCtrl, kRowMask>((int32_t)(uint32_t)((uint64_t)v >> 32));
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
+template <int kCtrl, int kRowMask, typename T>
+__device__ __forceinline__ T dpp_val(T v) {
+  if constexpr (sizeof(T) == 8) return (T)dpp_i64<kCtrl, kRowMask>((int64_t)v);
+  else return (T)dpp_i32<kCtrl, kRowMask>((int32_t)v);
+}
 __device__ __forceinline__ int64_t wave_sum_dpp(int64_t v) {
   v += dpp_i64<0xb1, 0xf>(v);
   v += dpp_i64<0x4e, 0xf>(v);
