@@ -75,52 +75,132 @@ __device__ __forceinline__ uint4 gene_payload(uint32_t g, uint8_t bt, uint8_t xf
   return *reinterpret_cast<const uint4*>(&gp);
 }
 
+// kEmitVec consecutive elements of a column for one lane: one 4- to 16-byte load in a full
+// tile (kFull: block-uniform, so no per-lane branches and no wait after every load), element
+// by element with zeros past n in the last tile.  The columns are allocated 16-byte aligned.
+constexpr int kEmitVec = 4;  // (the rank packing below assumes 4)
+template <bool kFull, typename T>
+__device__ __forceinline__ void load_vec(const T* __restrict__ col, int64_t p0, int64_t n, T (&v)[kEmitVec]) {
+  struct alignas(sizeof(T) * kEmitVec) Vec {
+    T x[kEmitVec];
+  };
+  if constexpr (kFull) {
+    const Vec w = *reinterpret_cast<const Vec*>(col + p0);
+#pragma unroll
+    for (int k = 0; k < kEmitVec; k++) v[k] = w.x[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < kEmitVec; k++) v[k] = p0 + k < n ? col[p0 + k] : (T)0;
+  }
+}
+
+// the columns gene_emit reads for one lane's kEmitVec consecutive records
+struct EmitIn {
+  int32_t g[kEmitVec];
+  uint8_t bt[kEmitVec], xf[kEmitVec], ug[kEmitVec], ul[kEmitVec];
+  uint16_t df[kEmitVec], gg[kEmitVec], gl[kEmitVec], gs[kEmitVec];
+  template <bool kFull>
+  __device__ __forceinline__ void load(const int32_t* __restrict__ gene, const RecCols& r,
+                                       const uint16_t* __restrict__ dflags, int64_t p0, int64_t n) {
+    load_vec<kFull>(gene, p0, n, g);
+    load_vec<kFull>(r.bits, p0, n, bt);
+    load_vec<kFull>(r.xf, p0, n, xf);
+    load_vec<kFull>(r.uy_gt30, p0, n, ug);
+    load_vec<kFull>(r.uy_len, p0, n, ul);
+    load_vec<kFull>(dflags, p0, n, df);
+    load_vec<kFull>(r.gq_gt30, p0, n, gg);
+    load_vec<kFull>(r.gq_len, p0, n, gl);
+    load_vec<kFull>(r.gq_sum, p0, n, gs);
+  }
+};
+
 // One block per kEmitTile records (input order, coalesced).  (1) rank every record among the
 // block's records of its gene bucket (wave-aggregated LDS counters); (2) reserve one range per
 // present bucket with one atomic on the bucket's cursor (k_gene_plan set it to the bucket's
 // start); (3) re-read the columns, build the payloads and write each at its range + rank.
-// The order inside a bucket region is therefore arbitrary; the reduction is order-free.
+// Each lane takes kEmitVec consecutive records per round, so every column is read with one
+// 4- to 16-byte load per lane (a wave covers 256 consecutive records per load); the ranks of
+// the lanes' k-th records are consecutive within a bucket, so the payload stores of one k
+// coalesce.  The order inside a bucket region is arbitrary; the reduction is order-free.
 constexpr int kEmitTile = 4 * kTile;
-constexpr int kEmitItems = kEmitTile / kBlock;
+constexpr int kEmitRounds = kEmitTile / (kBlock * kEmitVec);
+constexpr int kEmitBatch = 8;  // rounds whose gene loads are in flight together in pass 1
 static_assert(kEmitTile <= 65536, "ranks are 16-bit");
+static_assert(kEmitRounds % kEmitBatch == 0, "whole batches");
+
+template <bool kFull>
+__device__ __forceinline__ void gene_emit_tile(const int32_t* __restrict__ gene, const RecCols& r,
+                                               const uint16_t* __restrict__ dflags, int64_t n, int64_t base,
+                                               uint32_t* __restrict__ cursor, int n_buckets,
+                                               GenePayload* __restrict__ pay, uint32_t* s_cnt, uint32_t* s_off,
+                                               uint16_t* s_rank) {
+  const int t = threadIdx.x;
+  int nbb = 0;
+  while ((1 << nbb) < n_buckets) nbb++;
+  for (int i = t; i < n_buckets; i += kBlock) s_cnt[i] = 0;
+  __syncthreads();
+  // (1) ranks: a batch of rounds' gene vectors loaded together, then ranked
+  for (int j0 = 0; j0 < kEmitRounds; j0 += kEmitBatch) {
+    int32_t g[kEmitBatch][kEmitVec];
+#pragma unroll
+    for (int b = 0; b < kEmitBatch; b++) load_vec<kFull>(gene, base + ((j0 + b) * kBlock + t) * kEmitVec, n, g[b]);
+#pragma unroll
+    for (int b = 0; b < kEmitBatch; b++) {
+      const int q0 = ((j0 + b) * kBlock + t) * kEmitVec;
+      uint32_t rk[kEmitVec];
+#pragma unroll
+      for (int k = 0; k < kEmitVec; k++) {
+        const bool valid = kFull || base + q0 + k < n;
+        const uint32_t bk = valid ? (uint32_t)g[b][k] / kGenesPerBucket : 0u;
+        rk[k] = block_rank(bk, nbb, valid, s_cnt);
+      }
+      *reinterpret_cast<uint2*>(&s_rank[q0]) = make_uint2(rk[0] | (rk[1] << 16), rk[2] | (rk[3] << 16));
+    }
+  }
+  __syncthreads();
+  // (2) one range per present bucket
+  for (int i = t; i < n_buckets; i += kBlock) {
+    const uint32_t c = s_cnt[i];
+    if (c) s_off[i] = atomicAdd(&cursor[i], c);
+  }
+  __syncthreads();
+  // (3) payloads, software-pipelined: round j + 1's column loads are issued before round j's
+  // stores (vmcnt counts stores too, so loads issued after them would wait for them)
+  EmitIn cur;
+  cur.load<kFull>(gene, r, dflags, base + t * kEmitVec, n);
+#pragma unroll 2
+  for (int j = 0; j < kEmitRounds; j++) {
+    const int q0 = (j * kBlock + t) * kEmitVec;
+    const int64_t p0 = base + q0;
+    EmitIn nxt;
+    if (j + 1 < kEmitRounds) nxt.load<kFull>(gene, r, dflags, p0 + kBlock * kEmitVec, n);
+    const uint2 rp = *reinterpret_cast<const uint2*>(&s_rank[q0]);
+    const uint32_t rk[kEmitVec] = {rp.x & 0xffffu, rp.x >> 16, rp.y & 0xffffu, rp.y >> 16};
+#pragma unroll
+    for (int k = 0; k < kEmitVec; k++) {
+      if (kFull || p0 + k < n) {
+        const uint32_t gk = (uint32_t)cur.g[k];
+        const uint4 w = gene_payload(gk, cur.bt[k], cur.xf[k], cur.df[k], cur.ug[k], cur.ul[k], cur.gg[k],
+                                     cur.gl[k], cur.gs[k]);
+        reinterpret_cast<uint4*>(pay)[(uint64_t)s_off[gk / kGenesPerBucket] + rk[k]] = w;
+      }
+    }
+    if (j + 1 < kEmitRounds) cur = nxt;
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_gene_emit(const int32_t* __restrict__ gene, RecCols r,
                                                       const uint16_t* __restrict__ dflags, int64_t n,
                                                       uint32_t* __restrict__ cursor, int n_buckets,
                                                       GenePayload* __restrict__ pay) {
   uint32_t* s_cnt = sct_dyn_lds;              // n_buckets (dynamic LDS)
   uint32_t* s_off = sct_dyn_lds + n_buckets;  // n_buckets
-  __shared__ uint16_t s_rank[kEmitTile];
-  const int t = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) uint16_t s_rank[kEmitTile];
   const int64_t base = (int64_t)blockIdx.x * kEmitTile;
-  int nbb = 0;
-  while ((1 << nbb) < n_buckets) nbb++;
-  for (int i = t; i < n_buckets; i += kBlock) s_cnt[i] = 0;
-  __syncthreads();
-#pragma unroll 4
-  for (int j = 0; j < kEmitItems; j++) {
-    const int q = j * kBlock + t;
-    const int64_t p = base + q;
-    const bool valid = p < n;
-    const uint32_t bk = valid ? (uint32_t)gene[p] / kGenesPerBucket : 0u;
-    const uint32_t rank = block_rank(bk, nbb, valid, s_cnt);
-    s_rank[q] = (uint16_t)rank;
-  }
-  __syncthreads();
-  for (int i = t; i < n_buckets; i += kBlock) {
-    const uint32_t c = s_cnt[i];
-    if (c) s_off[i] = atomicAdd(&cursor[i], c);
-  }
-  __syncthreads();
-#pragma unroll 4
-  for (int j = 0; j < kEmitItems; j++) {
-    const int q = j * kBlock + t;
-    const int64_t p = base + q;
-    if (p >= n) break;
-    const uint32_t g = (uint32_t)gene[p];
-    const uint4 w = gene_payload(g, r.bits[p], r.xf[p], dflags[p], r.uy_gt30[p], r.uy_len[p], r.gq_gt30[p],
-                                 r.gq_len[p], r.gq_sum[p]);
-    reinterpret_cast<uint4*>(pay)[(uint64_t)s_off[g / kGenesPerBucket] + s_rank[q]] = w;
-  }
+  if (base + kEmitTile <= n)  // block-uniform
+    gene_emit_tile<true>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
+  else
+    gene_emit_tile<false>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
 }
 
 // one block: bucket starts (exclusive scan of the bucket counts) -> the emit cursors and the
