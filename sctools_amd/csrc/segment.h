@@ -134,15 +134,13 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
   const int64_t p0 = base + q0;
   const bool full = q0 + kItems <= tile_n;
   constexpr int ns = kCell ? 4 : 3;
-#pragma unroll 1
-  for (int st = 0; st < ns; st++) {
-    // numerator / denominator columns of stream st, kItems consecutive records, packed
+  // numerator / denominator columns of stream st, kItems consecutive records, packed
+  const auto load = [&](int st, uint32_t (&wn)[8], uint32_t (&wd)[8]) {
     const void* num = st == 0 ? (const void*)r.uy_gt30 : st == 1 ? (const void*)r.gq_gt30
                     : st == 2 ? (const void*)r.gq_sum : (const void*)r.cy_gt30;
     const void* den = st == 0 ? (const void*)r.uy_len : (st == 1 || st == 2) ? (const void*)r.gq_len
                     : (const void*)r.cy_len;
     const bool wide = (st == 1 || st == 2);  // uint16 columns
-    uint32_t wn[8], wd[8];
     if (full) {
       if (wide) {
         const uint4 a0 = reinterpret_cast<const uint4*>((const uint16_t*)num + p0)[0];
@@ -174,6 +172,14 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
         }
       }
     }
+  };
+  // stream st + 1's columns are loaded before stream st is summed (software pipeline)
+  uint32_t wn[8], wd[8], nn[8], nd[8];
+  load(0, wn, wd);
+#pragma unroll 1
+  for (int st = 0; st < ns; st++) {
+    const bool wide = (st == 1 || st == 2);
+    if (st + 1 < ns) load(st + 1, nn, nd);
     int64_t lanes[kStreamLanes];
 #pragma unroll
     for (int i = 0; i < kStreamLanes; i++) lanes[i] = 0;
@@ -193,6 +199,8 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
       fx_accumulate(lanes, ratio_rcp(a, d, s_rcp));
     }
     wave_flush<kStreamLanes>(lanes, cur_e >= 0, cur_e, partials, slot);
+#pragma unroll
+    for (int k = 0; k < 8; k++) wn[k] = nn[k], wd[k] = nd[k];
   }
 }
 
@@ -201,6 +209,9 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
 // global sort's (key with entity bits, u32 value with bit 31 = unmapped).
 // kStreams: also the exact quality-stream lanes of the runs (stream_tile), reusing the tile's
 // run ids: the stream ALU work overlaps the key pass's memory traffic in one launch.
+constexpr int kKeyBatch = 4;  // striped rounds whose column loads are issued together
+static_assert(kItems % kKeyBatch == 0, "whole batches");
+
 template <bool kCell, bool kGene, bool kBucket, bool kStreams>
 __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r, const uint8_t* __restrict__ k1_is_mito,
                                                            int64_t n, const uint64_t* __restrict__ tile_off, Bits b,
@@ -231,57 +242,75 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
   acc.clear();
   int64_t cur_e = -1;
   const auto slot = [](int i) { return A::slot(i); };
-  for (int j = 0; j < kItems; j++) {
-    const int q = j * kBlock + t;
-    const bool valid = q < tile_n;
-    const int64_t p = base + q;
-    const int64_t e = valid ? (int64_t)s_e[q] : cur_e;
-    wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
-    if (!valid) continue;
-    cur_e = e;
-    uint32_t k1 = (uint32_t)c.k1[p];
-    uint32_t k2 = (uint32_t)c.k2[p];
-    if (k1 >= c.n_k1 || k2 >= c.n_k2) {  // invalid input: reported, never used as an index
-      atomicOr(err, 2u);
-      k1 = k2 = 0;
+  // The columns of kKeyBatch rounds are loaded together (clamped, unconditional loads: all in
+  // flight at once), then the rounds are processed: the wait for memory is paid once per batch.
+  for (int j0 = 0; j0 < kItems; j0 += kKeyBatch) {
+    int32_t vk1[kKeyBatch], vk2[kKeyBatch], vref[kKeyBatch], vpos[kKeyBatch];
+    uint8_t vbt[kKeyBatch], vxf[kKeyBatch];
+#pragma unroll
+    for (int u = 0; u < kKeyBatch; u++) {
+      const int q = (j0 + u) * kBlock + t;
+      const int64_t p = base + (q < tile_n ? q : 0);
+      vk1[u] = c.k1[p];
+      vk2[u] = c.k2[p];
+      vbt[u] = r.bits[p];
+      vxf[u] = r.xf[p];
+      vref[u] = r.ref[p];
+      vpos[u] = r.pos[p];
     }
-    const uint8_t bt = r.bits[p];
-    const uint8_t xf = r.xf[p];
-    const bool mapped = !(bt & SCT_B_UNMAPPED);
-    const int32_t ref = r.ref[p];
-    const int32_t pos = r.pos[p];
-    const bool rev = bt & SCT_B_REVERSE;
-    const uint32_t hsh = mapped ? frag_hash(ref, pos, rev ? 1u : 0u) : 0u;
-    if constexpr (kBucket) {
-      const bool mito = kCell ? k1_is_mito[k1] != 0 : false;
-      keys[p] = payload_w0(make_key(0, k1, k2, hsh, b), ref, rev, mapped, mito);
-      static_cast<uint64_t*>(vals)[p] = ((uint64_t)p << 32) | (uint32_t)pos;
-      if (mapped && (uint32_t)ref >= (1u << kRefBits)) atomicOr(err, 1u);
-    } else {
-      keys[p] = make_key((uint64_t)e, k1, k2, hsh, b);
-      static_cast<uint32_t*>(vals)[p] = (uint32_t)p | (mapped ? 0u : kUnmappedValBit);
+#pragma unroll
+    for (int u = 0; u < kKeyBatch; u++) {
+      const int q = (j0 + u) * kBlock + t;
+      const bool valid = q < tile_n;
+      const int64_t p = base + q;
+      const int64_t e = valid ? (int64_t)s_e[q] : cur_e;
+      wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
+      if (!valid) continue;
+      cur_e = e;
+      uint32_t k1 = (uint32_t)vk1[u];
+      uint32_t k2 = (uint32_t)vk2[u];
+      if (k1 >= c.n_k1 || k2 >= c.n_k2) {  // invalid input: reported, never used as an index
+        atomicOr(err, 2u);
+        k1 = k2 = 0;
+      }
+      const uint8_t bt = vbt[u];
+      const uint8_t xf = vxf[u];
+      const bool mapped = !(bt & SCT_B_UNMAPPED);
+      const int32_t ref = vref[u];
+      const int32_t pos = vpos[u];
+      const bool rev = bt & SCT_B_REVERSE;
+      const uint32_t hsh = mapped ? frag_hash(ref, pos, rev ? 1u : 0u) : 0u;
+      if constexpr (kBucket) {
+        const bool mito = kCell ? k1_is_mito[k1] != 0 : false;
+        keys[p] = payload_w0(make_key(0, k1, k2, hsh, b), ref, rev, mapped, mito);
+        static_cast<uint64_t*>(vals)[p] = ((uint64_t)p << 32) | (uint32_t)pos;
+        if (mapped && (uint32_t)ref >= (1u << kRefBits)) atomicOr(err, 1u);
+      } else {
+        keys[p] = make_key((uint64_t)e, k1, k2, hsh, b);
+        static_cast<uint32_t*>(vals)[p] = (uint32_t)p | (mapped ? 0u : kUnmappedValBit);
+      }
+      // MetricAggregator.parse_molecule (aggregator.py:259-334)
+      acc.v[0] += 1;
+      acc.v[1] += (bt & SCT_B_PERFECT_UMI) ? 1 : 0;
+      if (mapped) {
+        const bool nh1 = bt & SCT_B_NH1;
+        acc.v[2] += (xf == SCT_XF_CODING);
+        acc.v[3] += (xf == SCT_XF_INTRONIC);
+        acc.v[4] += (xf == SCT_XF_UTR);
+        acc.v[5] += nh1 ? 1 : 0;
+        acc.v[6] += nh1 ? 0 : 1;
+        acc.v[7] += (bt & SCT_B_DUPLICATE) ? 1 : 0;
+        acc.v[8] += (bt & SCT_B_SPLICED) ? 1 : 0;
+      }
+      if constexpr (kCell) {
+        // CellMetrics.parse_extra_fields (aggregator.py:507-530) + mito reads (463-490)
+        acc.v[9] += ((bt & SCT_B_HAS_CB) && (bt & SCT_B_PERFECT_CB)) ? 1 : 0;
+        acc.v[10] += (xf == SCT_XF_INTERGENIC);
+        acc.v[11] += (xf == SCT_XF_ABSENT);
+        acc.v[12] += k1_is_mito[k1];
+      }
+      if (kGene) atomicAdd(&s_hist[k1 / kGenesPerBucket], 1u);
     }
-    // MetricAggregator.parse_molecule (aggregator.py:259-334)
-    acc.v[0] += 1;
-    acc.v[1] += (bt & SCT_B_PERFECT_UMI) ? 1 : 0;
-    if (mapped) {
-      const bool nh1 = bt & SCT_B_NH1;
-      acc.v[2] += (xf == SCT_XF_CODING);
-      acc.v[3] += (xf == SCT_XF_INTRONIC);
-      acc.v[4] += (xf == SCT_XF_UTR);
-      acc.v[5] += nh1 ? 1 : 0;
-      acc.v[6] += nh1 ? 0 : 1;
-      acc.v[7] += (bt & SCT_B_DUPLICATE) ? 1 : 0;
-      acc.v[8] += (bt & SCT_B_SPLICED) ? 1 : 0;
-    }
-    if constexpr (kCell) {
-      // CellMetrics.parse_extra_fields (aggregator.py:507-530) + mito reads (463-490)
-      acc.v[9] += ((bt & SCT_B_HAS_CB) && (bt & SCT_B_PERFECT_CB)) ? 1 : 0;
-      acc.v[10] += (xf == SCT_XF_INTERGENIC);
-      acc.v[11] += (xf == SCT_XF_ABSENT);
-      acc.v[12] += k1_is_mito[k1];
-    }
-    if (kGene) atomicAdd(&s_hist[k1 / kGenesPerBucket], 1u);
   }
   wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
   if (kGene) {
