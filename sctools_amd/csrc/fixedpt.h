@@ -58,24 +58,34 @@ SCT_HD uint64_t dbits(double x) {
 #endif
 }
 
-// Add X = x*2^68 and X^2 into 8 lanes (limb sums).  x must be 0 or >= 2^-16.
+// Add X = x*2^68 and X^2 into 8 lanes (limb sums).  x must be 0 or in [2^-16, 2^16).
+// The 53-bit significand is split as m = mh 2^32 + ml (mh < 2^21), so m^2 takes three 32x32
+// products instead of a general 64x64 multiply, and the shifts by s and 2s use the
+// (v >> 1) >> (63 - k) form, which needs no select for k == 0.
 SCT_HD void fx_accumulate(int64_t* lanes, double x) {
   const uint64_t b = dbits(x);
-  const int ex = (int)((b >> 52) & 0x7ff);
+  const uint32_t bhi = (uint32_t)(b >> 32);
+  const int ex = (int)((bhi >> 20) & 0x7ff);
   // x == 0 adds zeros (branch-free: m = 0, s = 0)
-  const uint64_t m = ex ? ((b & 0xFFFFFFFFFFFFFull) | (1ull << 52)) : 0ull;
+  const uint32_t mh = ex ? ((bhi & 0xFFFFFu) | 0x100000u) : 0u;
+  const uint32_t ml = ex ? (uint32_t)b : 0u;
   const int s = ex ? ex - 1007 : 0;  // X = m << s, 0 <= s <= 31
+  const uint64_t m = ((uint64_t)mh << 32) | ml;
   const uint64_t lo = m << s;
-  const uint64_t hi = s ? (m >> (64 - s)) : 0;
+  const uint32_t hi = (uint32_t)(((uint64_t)mh << s) >> 32);
   lanes[0] += (int64_t)(lo & 0xffffffffu);
   lanes[1] += (int64_t)(lo >> 32);
   lanes[2] += (int64_t)hi;
-  const uint64_t plo = m * m;
-  const uint64_t phi = umulhi64(m, m);
+  // m^2 = A + 2B 2^32 + C 2^64
+  const uint64_t A = (uint64_t)ml * ml;
+  const uint64_t B2 = ((uint64_t)ml * mh) << 1;  // < 2^54
+  const uint64_t C = (uint64_t)mh * mh;          // < 2^42
+  const uint64_t plo = A + (B2 << 32);
+  const uint64_t phi = C + (B2 >> 32) + (plo < A ? 1u : 0u);
   const int t = 2 * s;  // < 64
   const uint64_t w0 = plo << t;
-  const uint64_t w1 = t ? ((phi << t) | (plo >> (64 - t))) : phi;
-  const uint64_t w2 = t ? (phi >> (64 - t)) : 0;
+  const uint64_t w1 = (phi << t) | ((plo >> 1) >> (63 - t));
+  const uint64_t w2 = (phi >> 1) >> (63 - t);
   lanes[3] += (int64_t)(w0 & 0xffffffffu);
   lanes[4] += (int64_t)(w0 >> 32);
   lanes[5] += (int64_t)(w1 & 0xffffffffu);

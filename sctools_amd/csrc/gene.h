@@ -248,6 +248,12 @@ __global__ void __launch_bounds__(kBlock) k_gene_plan(const uint32_t* __restrict
   }
 }
 
+// s_sorted slot of sorted position i: within each group of 8 payloads (128 bytes) the slot is
+// XORed with the group index, so the 64 lanes reading their k-th payload (positions 8t + k)
+// spread over all 16-byte bank groups instead of 8-way conflicts.
+__device__ __forceinline__ uint32_t gswz(uint32_t i) { return i ^ ((i >> 3) & 7u); }
+static_assert(kGeneItems == 8, "gswz assumes 8 payloads per thread");
+
 struct GeneAcc {
   int32_t c[kGeneCnt];
   int64_t l[3 * kStreamLanes];
@@ -380,14 +386,14 @@ __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __res
 #pragma unroll
     for (int j = 0; j < kGeneItems; j++) {
       const int q = j * kBlock + t;
-      if (q < cnt) s_sorted[s_start[vx[j] - g0] + rk[j]] = src[sub + q];
+      if (q < cnt) s_sorted[gswz(s_start[vx[j] - g0] + rk[j])] = src[sub + q];
     }
     __syncthreads();
     // the thread's kGeneItems consecutive sorted payloads
     const int j0 = t * kGeneItems;
     const int my_n = cnt - j0 < 0 ? 0 : (cnt - j0 < kGeneItems ? cnt - j0 : kGeneItems);
     for (int k = 0; k < my_n; k++) {
-      const uint4 w = s_sorted[j0 + k];
+      const uint4 w = s_sorted[gswz(j0 + k)];
       const GenePayload& g = *reinterpret_cast<const GenePayload*>(&w);
       const int lg = (int)(g.gene - g0);
       if (lg != cur) {  // a gene boundary inside the thread's payloads: its own bin, no conflict

@@ -79,7 +79,12 @@ struct AddAcc {
   }
 };
 
-// Stage the tile's entity column, find run heads, and number the runs: s_e[q] = run index of
+// s_e holds one int per tile position with one pad word after every 16: the blocked passes
+// (thread t reads positions 16t .. 16t+15) then hit distinct banks instead of 16-way conflicts.
+__device__ __forceinline__ int epad(int q) { return q + (q >> 4); }
+constexpr int kTilePad = kTile + kTile / 16;
+
+// Stage the tile's entity column, find run heads, and number the runs: s_e[epad(q)] = run index of
 // tile position q.  Writes ent_start[run] for heads when ent_start is set.  Block-wide (barriers).
 __device__ __forceinline__ void tile_run_ids(const int32_t* __restrict__ ent, int64_t n, int64_t base, int tile_n,
                                              uint64_t tile_off, int32_t* s_e, int32_t* s_prev, uint64_t* s_scan,
@@ -88,19 +93,19 @@ __device__ __forceinline__ void tile_run_ids(const int32_t* __restrict__ ent, in
 #pragma unroll 4
   for (int j = 0; j < kItems; j++) {
     const int q = j * kBlock + t;
-    if (q < tile_n) s_e[q] = ent[base + q];
+    if (q < tile_n) s_e[epad(q)] = ent[base + q];
   }
   if (t == 0) *s_prev = base > 0 ? ent[base - 1] : 0;
   __syncthreads();
   const int q0 = t * kItems;
   uint32_t heads = 0;
   {
-    int32_t prev = q0 > 0 ? s_e[q0 - 1] : *s_prev;
+    int32_t prev = q0 > 0 ? s_e[epad(q0 - 1)] : *s_prev;
 #pragma unroll
     for (int j = 0; j < kItems; j++) {
       const int q = q0 + j;
       if (q < tile_n) {
-        const int32_t v = s_e[q];
+        const int32_t v = s_e[epad(q)];
         const bool h = (base + q == 0) || v != prev;
         heads |= (h ? 1u : 0u) << j;
         prev = v;
@@ -118,7 +123,7 @@ __device__ __forceinline__ void tile_run_ids(const int32_t* __restrict__ ent, in
       e += 1;
       if (ent_start) ent_start[e] = base + q;
     }
-    s_e[q] = (int32_t)e;
+    s_e[epad(q)] = (int32_t)e;
   }
   __syncthreads();
 }
@@ -190,7 +195,7 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
     for (int j = 0; j < kItems; j++) {
       const int q = q0 + j;
       const bool valid = q < tile_n;
-      const int64_t e = valid ? (int64_t)s_e[q] : cur_e;
+      const int64_t e = valid ? (int64_t)s_e[epad(q)] : cur_e;
       wave_flush<kStreamLanes>(lanes, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
       if (!valid) continue;
       cur_e = e;
@@ -209,7 +214,11 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
 // global sort's (key with entity bits, u32 value with bit 31 = unmapped).
 // kStreams: also the exact quality-stream lanes of the runs (stream_tile), reusing the tile's
 // run ids: the stream ALU work overlaps the key pass's memory traffic in one launch.
-constexpr int kKeyBatch = 4;  // striped rounds whose column loads are issued together
+#ifdef SCT_EXP_KB8
+constexpr int kKeyBatch = 8;
+#else
+constexpr int kKeyBatch = 4;
+#endif  // striped rounds whose column loads are issued together
 static_assert(kItems % kKeyBatch == 0, "whole batches");
 
 template <bool kCell, bool kGene, bool kBucket, bool kStreams>
@@ -221,7 +230,7 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
                                                            uint32_t* __restrict__ gene_counts, int n_buckets,
                                                            uint32_t* __restrict__ err) {
   static_assert(!kGene || kCell, "gene buckets come from the cell view");
-  __shared__ int32_t s_e[kTile];
+  __shared__ int32_t s_e[kTilePad];
   __shared__ int32_t s_prev;
   __shared__ uint64_t s_scan[kWaves + 1];
   uint32_t* s_hist = sct_dyn_lds;  // kGene: n_buckets counters (dynamic LDS)
@@ -263,7 +272,7 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
       const int q = (j0 + u) * kBlock + t;
       const bool valid = q < tile_n;
       const int64_t p = base + q;
-      const int64_t e = valid ? (int64_t)s_e[q] : cur_e;
+      const int64_t e = valid ? (int64_t)s_e[epad(q)] : cur_e;
       wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
       if (!valid) continue;
       cur_e = e;
