@@ -214,11 +214,7 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
 // global sort's (key with entity bits, u32 value with bit 31 = unmapped).
 // kStreams: also the exact quality-stream lanes of the runs (stream_tile), reusing the tile's
 // run ids: the stream ALU work overlaps the key pass's memory traffic in one launch.
-#ifdef SCT_EXP_KB8
-constexpr int kKeyBatch = 8;
-#else
-constexpr int kKeyBatch = 4;
-#endif  // striped rounds whose column loads are issued together
+constexpr int kKeyBatch = 4;  // striped rounds whose column loads are issued together (8: occupancy 3, slower)
 static_assert(kItems % kKeyBatch == 0, "whole batches");
 
 template <bool kCell, bool kGene, bool kBucket, bool kStreams>
