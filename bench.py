@@ -53,6 +53,10 @@ ALG_BYTES = {
 }
 
 
+# HIP-event kernel names (engine profile) -> rocprofv3 kernel names (tools/pmc_traffic.py keys)
+PMC_NAMES = {"build_keys": "build_keys_run", "scan": "scan_wide"}
+
+
 def pipeline_bytes(args, dims):
     """B_alg = 32 + 12 + 24 P + 44 bytes/record, P = ceil(b / 8) LSD passes with
     b = bits(cells per shard) + bits(gene ids) + bits(umi ids) -- a property of the workload."""
@@ -262,6 +266,7 @@ def pmc_traffic(args, kernel):
     if not path or not os.path.exists(path) or args.records != 100_000_000 or args.cells != 10_000:
         return None
     d = json.load(open(path))
+    kernel = PMC_NAMES.get(kernel, kernel)
     if d.get("source_sha256") != source_hash(ROOT) or kernel not in d.get("kernels", {}):
         return None
     return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
