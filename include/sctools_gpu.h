@@ -286,8 +286,11 @@ int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void*
  * HIP events on its launch stream.  sct_profile_read waits for the events,
  * fills up to `max_kernels` (name, total ms, launches) triples (host arrays;
  * names stay valid until the next read), resets, and returns the number of
- * distinct kernels seen.  Thread-local. */
+ * distinct kernels seen.  sct_profile_only restricts the timing to the kernels
+ * of one name (NULL or "": all kernels), so a caller can time one kernel
+ * without bracketing every launch.  Thread-local. */
 int sct_profile_enable(int on);
+int sct_profile_only(const char* kernel_name);
 int sct_profile_read(const char** names, double* ms, int64_t* launches, int max_kernels);
 
 #ifdef __cplusplus

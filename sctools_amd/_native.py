@@ -34,8 +34,8 @@ RECORD_COLUMNS = ("cell", "umi", "gene", "ref", "pos", "gq_sum", "gq_len", "gq_g
 
 EXPORTED = ("sct_abi_version", "sct_last_error", "sct_workspace_size", "sct_count_entities",
             "sct_compute_metrics", "sct_gene_partials", "sct_cell_metrics_gene_partials",
-            "sct_finalize_partials", "sct_profile_enable", "sct_profile_read", "sct_tag_sort_workspace_size",
-            "sct_tag_sort", "sct_verify_sort", "sct_count_matrix_workspace_size", "sct_count_matrix")
+            "sct_finalize_partials", "sct_profile_enable", "sct_profile_only", "sct_profile_read",
+            "sct_tag_sort_workspace_size", "sct_tag_sort", "sct_verify_sort", "sct_count_matrix_workspace_size", "sct_count_matrix")
 ORDER_CELL, ORDER_CELL_UMI_GENE, ORDER_GENE_CELL_UMI = 0, 1, 2
 PLAN_GENE_PARTIALS = 0x1
 
@@ -142,6 +142,8 @@ def load() -> ctypes.CDLL:
     L.sct_count_matrix.argtypes = [ctypes.POINTER(CountInput), ctypes.POINTER(CountOutput), vp, ctypes.c_size_t, vp]
     L.sct_profile_enable.restype = ctypes.c_int
     L.sct_profile_enable.argtypes = [ctypes.c_int]
+    L.sct_profile_only.restype = ctypes.c_int
+    L.sct_profile_only.argtypes = [ctypes.c_char_p]
     L.sct_profile_read.restype = ctypes.c_int
     L.sct_profile_read.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(i64), ctypes.c_int]

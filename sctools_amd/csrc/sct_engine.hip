@@ -573,6 +573,11 @@ int sct_profile_enable(int on) {
   return SCT_OK;
 }
 
+int sct_profile_only(const char* kernel_name) {
+  prof_only() = kernel_name ? kernel_name : "";
+  return SCT_OK;
+}
+
 int sct_profile_read(const char** names, double* ms, int64_t* launches, int max_kernels) {
   // waits for the recorded events, returns per-kernel totals, and resets the counters
   static thread_local std::vector<std::string> held;

@@ -52,6 +52,11 @@ inline bool& prof_on() {
   static thread_local bool on = false;
   return on;
 }
+inline std::string& prof_only() {  // "" = every kernel
+  static thread_local std::string name;
+  return name;
+}
+inline bool prof_wants(const char* n) { return prof_on() && (prof_only().empty() || prof_only() == n); }
 inline std::vector<ProfEntry>& prof_entries() {
   static thread_local std::vector<ProfEntry> v;
   return v;
@@ -62,10 +67,11 @@ struct ProfScope {
   hipStream_t s;
   const char* name;
   ProfScope(const char* n, hipStream_t st) : s(st), name(n) {
-    if (prof_on() && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess) (void)hipEventRecord(a, s);
+    if (prof_wants(n) && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+      (void)hipEventRecord(a, s);
   }
   ~ProfScope() {
-    if (!prof_on() || !a || !b) return;
+    if (!a || !b) return;
     (void)hipEventRecord(b, s);
     for (auto& e : prof_entries())
       if (e.name == name) {

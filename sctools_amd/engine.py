@@ -261,6 +261,10 @@ class Engine:
     def profile_enable(self, on: bool = True):
         self.lib.sct_profile_enable(1 if on else 0)
 
+    def profile_only(self, kernel: str = ""):
+        """Time only the launches of `kernel` ("" = all) while profiling is enabled."""
+        self.lib.sct_profile_only(kernel.encode())
+
     def profile_read(self) -> Dict[str, Tuple[float, int]]:
         cap = 64
         names = (ctypes.c_char_p * cap)()
