@@ -273,13 +273,12 @@ struct GeneAcc {
     fx_accumulate(l + 1 * kStreamLanes, ratio_rcp(g.gq_gt30, g.gq_len, s_rcp));
     fx_accumulate(l + 2 * kStreamLanes, ratio_rcp(g.gq_sum, g.gq_len, s_rcp));
   }
+  // unconditional adds (zeros included): a per-lane test would cost an exec-mask round per lane
   __device__ __forceinline__ void flush(int32_t* cbin, unsigned long long* lbin) const {
 #pragma unroll
-    for (int i = 0; i < kGeneCnt; i++)
-      if (c[i]) atomicAdd(&cbin[i], c[i]);
+    for (int i = 0; i < kGeneCnt; i++) atomicAdd(&cbin[i], c[i]);
 #pragma unroll
-    for (int i = 0; i < 3 * kStreamLanes; i++)
-      if (l[i]) atomicAdd(&lbin[i], (unsigned long long)l[i]);
+    for (int i = 0; i < 3 * kStreamLanes; i++) atomicAdd(&lbin[i], (unsigned long long)l[i]);
   }
 };
 
