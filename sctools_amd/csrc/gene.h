@@ -254,33 +254,55 @@ __global__ void __launch_bounds__(kBlock) k_gene_plan(const uint32_t* __restrict
 __device__ __forceinline__ uint32_t gswz(uint32_t i) { return i ^ ((i >> 3) & 7u); }
 static_assert(kGeneItems == 8, "gswz assumes 8 payloads per thread");
 
+// Bit i of an 8-bit value moved to bit 4i (nibble i) of a 32-bit word.
+__device__ __forceinline__ uint32_t spread_nibbles(uint32_t x) {
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  return (x | (x << 3)) & 0x11111111u;
+}
+
+// A thread's run of one gene.  The 16 flag bits are counted in nibbles of pk (a run collects at
+// most kGeneItems <= 15 payloads before it is flushed), two adds per payload instead of one
+// extract-and-add per flag; counts() expands them into the kGeneCnt counter lanes.
 struct GeneAcc {
-  int32_t c[kGeneCnt];
+  uint32_t pk[2];  // nibble f of pk[f / 8]: #payloads with flag bit f
+  int32_t n;       // n_reads
   int64_t l[3 * kStreamLanes];
   __device__ __forceinline__ void clear() {
-#pragma unroll
-    for (int i = 0; i < kGeneCnt; i++) c[i] = 0;
+    pk[0] = pk[1] = 0;
+    n = 0;
 #pragma unroll
     for (int i = 0; i < 3 * kStreamLanes; i++) l[i] = 0;
   }
   __device__ __forceinline__ void add(const GenePayload& g, const double* s_rcp) {
-    c[0] += 1;
-#pragma unroll
-    for (int f = 0; f < kGeneFlags; f++) c[1 + f] += (g.flags >> f) & 1u;
-    c[1 + 9] -= (g.flags >> 14) & 1u;   // GF_MOL_SECOND on the GF_MOL_SINGLE lane
-    c[1 + 11] -= (g.flags >> 15) & 1u;  // GF_FRAG_SECOND on the GF_FRAG_SINGLE lane
+    n += 1;
+    pk[0] += spread_nibbles(g.flags & 0xffu);
+    pk[1] += spread_nibbles((uint32_t)g.flags >> 8);
     fx_accumulate(l + 0 * kStreamLanes, ratio_rcp(g.uy_gt30, g.uy_len, s_rcp));
     fx_accumulate(l + 1 * kStreamLanes, ratio_rcp(g.gq_gt30, g.gq_len, s_rcp));
     fx_accumulate(l + 2 * kStreamLanes, ratio_rcp(g.gq_sum, g.gq_len, s_rcp));
   }
+  // counter lanes: n_reads, then flag f on lane 1 + f; GF_MOL_SECOND (bit 14) and GF_FRAG_SECOND
+  // (bit 15) subtract from the GF_MOL_SINGLE / GF_FRAG_SINGLE lanes
+  __device__ __forceinline__ void counts(int32_t (&c)[kGeneCnt]) const {
+    c[0] = n;
+#pragma unroll
+    for (int f = 0; f < kGeneFlags; f++) c[1 + f] = (int32_t)((pk[f / 8] >> (4 * (f % 8))) & 0xfu);
+    c[1 + 9] -= (int32_t)((pk[1] >> 24) & 0xfu);
+    c[1 + 11] -= (int32_t)(pk[1] >> 28);
+  }
   // unconditional adds (zeros included): a per-lane test would cost an exec-mask round per lane
   __device__ __forceinline__ void flush(int32_t* cbin, unsigned long long* lbin) const {
+    int32_t c[kGeneCnt];
+    counts(c);
 #pragma unroll
     for (int i = 0; i < kGeneCnt; i++) atomicAdd(&cbin[i], c[i]);
 #pragma unroll
     for (int i = 0; i < 3 * kStreamLanes; i++) atomicAdd(&lbin[i], (unsigned long long)l[i]);
   }
 };
+static_assert(kGeneItems <= 15, "nibble counters");
+static_assert(kGeneFlags == 14, "flag bits 14 and 15 are the SECOND events");
 
 // Segmented inclusive DPP scan of one value over the wave: lanes hold partial sums of the
 // segment (contiguous lanes with equal keys) that starts at lane `seg`; m[0..5] say whether
@@ -317,12 +339,21 @@ __device__ __forceinline__ void gene_wave_flush(GeneAcc& acc, int key, int32_t* 
   const uint64_t upto = lane == kWave - 1 ? ~0ull : ((1ull << (lane + 1)) - 1);
   const int seg = kWave - 1 - __clzll((unsigned long long)(heads & upto));
   const bool m[6] = {seg <= lane - 1, seg <= lane - 2, seg <= lane - 4, seg <= lane - 8, seg < (lane & ~15), seg <= 31};
+  int32_t c[kGeneCnt];
+  acc.counts(c);
 #pragma unroll
-  for (int i = 0; i < kGeneCnt; i++) acc.c[i] = seg_scan_dpp(acc.c[i], m);
+  for (int i = 0; i < kGeneCnt; i++) c[i] = seg_scan_dpp(c[i], m);
 #pragma unroll
   for (int i = 0; i < 3 * kStreamLanes; i++) acc.l[i] = seg_scan_dpp(acc.l[i], m);
   const bool tail = lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull);
-  if (tail && key >= 0) acc.flush(&s_cbin[key * kGeneCntPad], &s_lbin[key * 3 * kStreamLanes]);
+  if (tail && key >= 0) {
+    int32_t* cb = &s_cbin[key * kGeneCntPad];
+    unsigned long long* lb = &s_lbin[key * 3 * kStreamLanes];
+#pragma unroll
+    for (int i = 0; i < kGeneCnt; i++) atomicAdd(&cb[i], c[i]);
+#pragma unroll
+    for (int i = 0; i < 3 * kStreamLanes; i++) atomicAdd(&lb[i], (unsigned long long)acc.l[i]);
+  }
 }
 
 // One work item = (gene bucket, range of its payloads).  Each sub-tile of kGeneSub payloads is
