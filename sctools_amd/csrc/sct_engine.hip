@@ -368,8 +368,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   if (gene) HIPCHK(hipMemsetAsync(gcounts, 0, sizeof(uint32_t) * (size_t)L.n_buckets, s));
 
   // 1. input order: runs, keys, additive metrics (+ gene-bucket counts per tile)
-  const int64_t tiles = cdiv(n, kTile);
-  const dim3 tgrid((unsigned)tiles);
+  const dim3 tgrid((unsigned)cdiv(n, kKTile));  // key-pass blocks (tile offsets are per kTile)
   const uint64_t* toff = at<uint64_t>(ws, L.tile_cnt);
   // exact mean / variance lanes of the output rows ride along in the same launch
   const bool streams = exact && out_i;

@@ -82,7 +82,14 @@ struct AddAcc {
 // s_e holds one int per tile position with one pad word after every 16: the blocked passes
 // (thread t reads positions 16t .. 16t+15) then hit distinct banks instead of 16-way conflicts.
 __device__ __forceinline__ int epad(int q) { return q + (q >> 4); }
-constexpr int kTilePad = kTile + kTile / 16;
+// The key pass (k_build_keys_run) owns kKTile records per block, kKItems per thread: twice the
+// heads tile (k_heads / tile offsets are per kTile), which halves the per-block costs (run-id
+// scan, the wave flushes that end each quality stream, the gene-bucket histogram flush).
+constexpr int kKItems = 2 * kItems;  // 32: the blocked head masks are 32-bit
+constexpr int kKTile = kBlock * kKItems;
+constexpr int kKTilesPerBlock = kKTile / kTile;
+constexpr int kTilePad = kKTile + kKTile / 16;
+static_assert(kKItems <= 32, "head masks are 32-bit");
 
 // Stage the tile's entity column, find run heads, and number the runs: s_e[epad(q)] = run index of
 // tile position q.  Writes ent_start[run] for heads when ent_start is set.  Block-wide (barriers).
@@ -91,18 +98,18 @@ __device__ __forceinline__ void tile_run_ids(const int32_t* __restrict__ ent, in
                                              int64_t* __restrict__ ent_start) {
   const int t = threadIdx.x;
 #pragma unroll 4
-  for (int j = 0; j < kItems; j++) {
+  for (int j = 0; j < kKItems; j++) {
     const int q = j * kBlock + t;
     if (q < tile_n) s_e[epad(q)] = ent[base + q];
   }
   if (t == 0) *s_prev = base > 0 ? ent[base - 1] : 0;
   __syncthreads();
-  const int q0 = t * kItems;
+  const int q0 = t * kKItems;
   uint32_t heads = 0;
   {
     int32_t prev = q0 > 0 ? s_e[epad(q0 - 1)] : *s_prev;
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < kKItems; j++) {
       const int q = q0 + j;
       if (q < tile_n) {
         const int32_t v = s_e[epad(q)];
@@ -116,7 +123,7 @@ __device__ __forceinline__ void tile_run_ids(const int32_t* __restrict__ ent, in
   const uint64_t ex = block_exclusive_scan<uint64_t>((uint64_t)__popc(heads), &tot, s_scan);  // has barriers
   int64_t e = (int64_t)(tile_off + ex) - 1;
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
+  for (int j = 0; j < kKItems; j++) {
     const int q = q0 + j;
     if (q >= tile_n) break;
     if (heads & (1u << j)) {
@@ -135,12 +142,12 @@ template <bool kCell>
 __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int tile_n, const int32_t* s_e,
                                             const double* s_rcp, int64_t* __restrict__ partials) {
   const int t = threadIdx.x;
-  const int q0 = t * kItems;
-  const int64_t p0 = base + q0;
-  const bool full = q0 + kItems <= tile_n;
   constexpr int ns = kCell ? 4 : 3;
-  // numerator / denominator columns of stream st, kItems consecutive records, packed
-  const auto load = [&](int st, uint32_t (&wn)[8], uint32_t (&wd)[8]) {
+  // numerator / denominator columns of half h of stream st: items q0 .. q0 + kItems - 1 of the thread's kKItems
+  const auto load = [&](int st, int h, uint32_t (&wn)[8], uint32_t (&wd)[8]) {
+    const int q0 = t * kKItems + h * kItems;
+    const int64_t p0 = base + q0;
+    const bool full = q0 + kItems <= tile_n;
     const void* num = st == 0 ? (const void*)r.uy_gt30 : st == 1 ? (const void*)r.gq_gt30
                     : st == 2 ? (const void*)r.gq_sum : (const void*)r.cy_gt30;
     const void* den = st == 0 ? (const void*)r.uy_len : (st == 1 || st == 2) ? (const void*)r.gq_len
@@ -178,17 +185,23 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
       }
     }
   };
-  // stream st + 1's columns are loaded before stream st is summed (software pipeline)
+  int64_t lanes[kStreamLanes];
+  int64_t cur_e = -1;
+  // the next (stream, half)'s columns are loaded before the current one is summed (software
+  // pipeline); a stream's lanes run over both halves and are flushed once
   uint32_t wn[8], wd[8], nn[8], nd[8];
-  load(0, wn, wd);
+  load(0, 0, wn, wd);
 #pragma unroll 1
-  for (int st = 0; st < ns; st++) {
+  for (int sh = 0; sh < 2 * ns; sh++) {
+    const int st = sh >> 1, h = sh & 1;
     const bool wide = (st == 1 || st == 2);
-    if (st + 1 < ns) load(st + 1, nn, nd);
-    int64_t lanes[kStreamLanes];
+    if (sh + 1 < 2 * ns) load((sh + 1) >> 1, (sh + 1) & 1, nn, nd);
+    const int q0 = t * kKItems + h * kItems;
+    if (h == 0) {
 #pragma unroll
-    for (int i = 0; i < kStreamLanes; i++) lanes[i] = 0;
-    int64_t cur_e = -1;
+      for (int i = 0; i < kStreamLanes; i++) lanes[i] = 0;
+      cur_e = -1;
+    }
     const int slot0 = P_FLOAT + st * kStreamLanes;
     const auto slot = [slot0](int i) { return slot0 + i; };
 #pragma unroll
@@ -203,7 +216,7 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
       const uint32_t d = wide ? (wd[j / 2] >> (16 * (j % 2))) & 0xffffu : (wd[j / 4] >> (8 * (j % 4))) & 0xffu;
       fx_accumulate(lanes, ratio_rcp(a, d, s_rcp));
     }
-    wave_flush<kStreamLanes>(lanes, cur_e >= 0, cur_e, partials, slot);
+    if (h == 1) wave_flush<kStreamLanes>(lanes, cur_e >= 0, cur_e, partials, slot);
 #pragma unroll
     for (int k = 0; k < 8; k++) wn[k] = nn[k], wd[k] = nd[k];
   }
@@ -215,7 +228,7 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
 // kStreams: also the exact quality-stream lanes of the runs (stream_tile), reusing the tile's
 // run ids: the stream ALU work overlaps the key pass's memory traffic in one launch.
 constexpr int kKeyBatch = 4;  // striped rounds whose column loads are issued together (8: occupancy 3, slower)
-static_assert(kItems % kKeyBatch == 0, "whole batches");
+static_assert(kKItems % kKeyBatch == 0, "whole batches");
 
 template <bool kCell, bool kGene, bool kBucket, bool kStreams>
 __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r, const uint8_t* __restrict__ k1_is_mito,
@@ -232,13 +245,14 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
   uint32_t* s_hist = sct_dyn_lds;  // kGene: n_buckets counters (dynamic LDS)
   __shared__ double s_rcp[kStreams ? kRcpN : 1];
   const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kTile;
-  const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
+  const int64_t base = (int64_t)blockIdx.x * kKTile;
+  const int tile_n = (int)((n - base) < kKTile ? (n - base) : kKTile);
   if (kGene)
     for (int i = t; i < n_buckets; i += kBlock) s_hist[i] = 0;
   if (kStreams) fill_rcp(s_rcp);  // visible after tile_run_ids' barriers
   // 1-2. run index of every record of the tile
-  tile_run_ids(c.ent, n, base, tile_n, tile_off[blockIdx.x], s_e, &s_prev, s_scan, ent_start);
+  tile_run_ids(c.ent, n, base, tile_n, tile_off[(size_t)blockIdx.x * kKTilesPerBlock], s_e, &s_prev, s_scan,
+               ent_start);
 
   // 3. striped pass: keys, values and the run's additive metrics.  Runs are contiguous, so
   // in a round the wave's lanes cross a run boundary together: flush wave-cooperatively.
@@ -249,7 +263,7 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
   const auto slot = [](int i) { return A::slot(i); };
   // The columns of kKeyBatch rounds are loaded together (clamped, unconditional loads: all in
   // flight at once), then the rounds are processed: the wait for memory is paid once per batch.
-  for (int j0 = 0; j0 < kItems; j0 += kKeyBatch) {
+  for (int j0 = 0; j0 < kKItems; j0 += kKeyBatch) {
     int32_t vk1[kKeyBatch], vk2[kKeyBatch], vref[kKeyBatch], vpos[kKeyBatch];
     uint8_t vbt[kKeyBatch], vxf[kKeyBatch];
 #pragma unroll
