@@ -67,7 +67,7 @@ __device__ __forceinline__ uint64_t make_key(uint64_t e, uint32_t k1, uint32_t k
 template <bool kCell>
 struct AddAcc {
   static constexpr int kK = kCell ? 13 : 9;
-  int64_t v[kK];
+  int32_t v[kK];  // per thread: at most kKItems records between flushes
   // counter i -> partial slot: 0..8 are P_N_READS..P_SPLICED; 9..12 are P_PERFECT_CB, P_INTERGENIC,
   // P_UNMAPPED, P_MITO_READS
   static __device__ __forceinline__ int slot(int i) {

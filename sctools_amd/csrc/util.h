@@ -292,6 +292,15 @@ __device__ __forceinline__ int64_t wave_sum_dpp(int64_t v) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// Sum over the wave of an int64 value with |v| < 2^49 on every lane: the low 24 bits and the
+// (arithmetic) rest are summed as two int32 DPP reductions, which cannot overflow (64 lanes:
+// < 2^30 and < 2^31), instead of a carry-propagating 64-bit DPP add per step.
+__device__ __forceinline__ int64_t wave_sum_dpp_split(int64_t v) {
+  const int32_t lo = (int32_t)(v & 0xFFFFFF);
+  const int32_t hi = (int32_t)(v >> 24);
+  return (int64_t)wave_sum_dpp(lo) + ((int64_t)wave_sum_dpp(hi) << 24);
+}
+
 // Wave-cooperative flush of per-lane partial sums into int64 rows.
 //
 // Lanes with `member` set hold partial sums v[0..K) for entity `e` (per lane).  For every
@@ -299,7 +308,8 @@ __device__ __forceinline__ int64_t wave_sum_dpp(int64_t v) {
 // is inside one entity), the members' values are summed across the wave (DPP) and lanes
 // 0..K-1 add slot SlotOf(i) of that entity's row with ONE atomic instruction instead of K
 // single-lane instructions per lane.  Members' v[] are cleared.  Every lane of the wave must
-// call it with all lanes active.  T = int32_t or int64_t.
+// call it with all lanes active.  T = int32_t, or int64_t with |v| < 2^49 per lane (the key
+// pass's fixed-point lanes: < 2^45 for 32 records).
 template <int K, typename T, typename SlotOf>
 __device__ __forceinline__ void wave_flush(T (&v)[K], bool member, int64_t e, int64_t* __restrict__ rows,
                                            SlotOf slot_of) {
@@ -313,7 +323,9 @@ __device__ __forceinline__ void wave_flush(T (&v)[K], bool member, int64_t e, in
     int64_t mine = 0;
 #pragma unroll
     for (int i = 0; i < K; i++) {
-      const T tot = wave_sum_dpp(in ? v[i] : (T)0);
+      T tot;
+      if constexpr (sizeof(T) == 8) tot = (T)wave_sum_dpp_split(in ? (int64_t)v[i] : 0);
+      else tot = wave_sum_dpp(in ? v[i] : (T)0);
       mine = (lane == i) ? (int64_t)tot : mine;
     }
     if (lane < K && mine) atomicAdd((unsigned long long*)&rows[el * SCT_NP + slot_of(lane)], (unsigned long long)mine);
