@@ -452,10 +452,12 @@ __global__ void __launch_bounds__(kHBlock) k_hash_tile(const uint16_t* __restric
     const uint64_t x0 = pb ? w0_b[w0 + q] : w0_a[w0 + q];
     const uint64_t x1 = pb ? w1_b[w0 + q] : w1_a[w0 + q];
     const uint64_t key = (x0 >> kKeyShift) & kmask;  // ids >= the dictionary sizes stay inside KB bits
-    int ek, em, ef = 0;
-    ht_insert<K1E>(s_k1, (K1E)((((uint64_t)bs << b.k1) | (key >> sh_k1)) << 2), ek);
+    int ek = 0, em, ef = 0;
     const uint32_t ms =
         ht_insert<unsigned long long>(s_mol, (((uint64_t)bs << mol_bits) | (key >> sh_mol)) << 2, em);
+    // A record whose molecule already had two records (em == 0) cannot change the (bucket, k1)
+    // events: that group's inserter and first finder are among the molecule's first two records.
+    if (em != 0) ht_insert<K1E>(s_k1, (K1E)((((uint64_t)bs << b.k1) | (key >> sh_k1)) << 2), ek);
     if (x0 & kW0Mapped) {
       const uint64_t fk = ((((uint64_t)ms << 18) | payload_frag(x0)) << 32) | (uint32_t)x1;
       ht_insert<unsigned long long>(s_frg, fk << 2, ef);
@@ -526,9 +528,9 @@ __global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict_
     const uint64_t x0 = W0[g.start + p];
     const uint64_t x1 = W1[g.start + p];
     const uint64_t key = (x0 >> kKeyShift) & kmask;
-    int ek, em, ef = 0;
-    ht_insert<K1E>(s_k1, (K1E)((key >> sh_k1) << 2), ek, tb);
+    int ek = 0, em, ef = 0;
     const uint32_t ms = ht_insert<unsigned long long>(s_mol, (key >> sh_mol) << 2, em, tb);
+    if (em != 0) ht_insert<K1E>(s_k1, (K1E)((key >> sh_k1) << 2), ek, tb);  // as in k_hash_tile
     if (x0 & kW0Mapped) {
       const uint64_t fk = ((((uint64_t)ms << 18) | payload_frag(x0)) << 32) | (uint32_t)x1;
       ht_insert<unsigned long long>(s_frg, fk << 2, ef, tb);
