@@ -249,11 +249,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (SURVEY.md 8(d) config-2 generator, generated on GPU)",
+            "data": "synthetic (SURVEY.md 8(d) config-%d generator, generated on GPU)" % args.config,
             "config": {
                 "workload": ({2: "config2: %d cell-sorted records/rank",
                               4: "config4: %d cell-sorted records/rank, lognormal(0, 2) reads per cell",
-                              5: "config5: %d globally shuffled records/rank (30%% NH>1, 40%% dup), GPU sort by cell + "}
+                              5: "config5: %d globally shuffled records/rank (30%% NH>1, 40%% dup), GPU sort by cell"}
                              [args.config]) % args.records + ", %d cells/rank, %d genes; cell metrics + grouped gene metrics%s"
                             % (args.cells, args.genes, " + RCCL all-reduce" if world > 1 else ""),
                 "records_per_rank": args.records,
