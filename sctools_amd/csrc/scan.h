@@ -39,26 +39,60 @@ __global__ void k_scan_small(uint64_t* __restrict__ data, int64_t m, uint64_t* _
   if (threadIdx.x == 0 && out_total) *out_total = carry;
 }
 
-// one 1024-thread block: exclusive scan of m uint64 in place, each thread owning a contiguous
-// run of elements (a few tens of microseconds faster than k_scan_small's 256-wide sweeps at
-// ~25K elements); the total goes to *out_total (if set)
+// one 1024-thread block: exclusive scan of m uint64 in place (the per-tile run counts, ~25K
+// elements at 100M records).  Chunks of kScanWChunk are loaded coalesced (the next chunk's
+// loads in flight while the current one is scanned), transposed through LDS so each thread
+// scans kScanPer consecutive elements, and stored coalesced; the total goes to *out_total.
+// (Each thread walking its own contiguous run straight from HBM serialised ~24 dependent
+// loads per thread: 45-240 us.)
 constexpr int kScanWide = 1024;
+constexpr int kScanPer = 4;
+constexpr int kScanWChunk = kScanWide * kScanPer;  // 32 KB of LDS
 __global__ void __launch_bounds__(kScanWide) k_scan_wide(uint64_t* __restrict__ data, int64_t m,
                                                          uint64_t* __restrict__ out_total) {
+  __shared__ uint64_t s_v[kScanWChunk];
   __shared__ uint64_t lds[kScanWide / kWave + 1];
-  const int64_t per = (m + kScanWide - 1) / kScanWide;
-  const int64_t b = (int64_t)threadIdx.x * per;
-  const int64_t e = b + per < m ? b + per : m;
-  uint64_t s = 0;
-  for (int64_t i = b; i < e; i++) s += data[i];
-  uint64_t tot;
-  uint64_t run = block_exclusive_scan_n<kScanWide, uint64_t>(s, &tot, lds);
-  for (int64_t i = b; i < e; i++) {
-    const uint64_t v = data[i];
-    data[i] = run;
-    run += v;
+  const int t = threadIdx.x;
+  uint64_t nxt[kScanPer];
+#pragma unroll
+  for (int k = 0; k < kScanPer; k++) {
+    const int64_t p = (int64_t)k * kScanWide + t;
+    nxt[k] = p < m ? data[p] : 0;
   }
-  if (threadIdx.x == 0 && out_total) *out_total = tot;
+  uint64_t carry = 0;
+  for (int64_t base = 0; base < m; base += kScanWChunk) {
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) s_v[k * kScanWide + t] = nxt[k];
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) {
+      const int64_t p = base + kScanWChunk + (int64_t)k * kScanWide + t;
+      nxt[k] = p < m ? data[p] : 0;
+    }
+    __syncthreads();
+    uint64_t v[kScanPer];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) {
+      v[k] = s_v[t * kScanPer + k];
+      sum += v[k];
+    }
+    uint64_t tot;
+    uint64_t run = carry + block_exclusive_scan_n<kScanWide, uint64_t>(sum, &tot, lds);
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) {
+      s_v[t * kScanPer + k] = run;
+      run += v[k];
+    }
+    carry += tot;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) {
+      const int64_t p = base + (int64_t)k * kScanWide + t;
+      if (p < m) data[p] = s_v[k * kScanWide + t];
+    }
+    __syncthreads();  // the next chunk overwrites s_v
+  }
+  if (t == 0 && out_total) *out_total = carry;
 }
 
 __global__ void k_scan_apply(const uint32_t* __restrict__ in, int64_t m, const uint64_t* __restrict__ block_off,

@@ -150,7 +150,11 @@ int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool du
     HIPCHK(hipMemsetAsync(seen, 0, sizeof(uint32_t) * (size_t)n_ids, s));
   }
   HIPCHK(hipMemsetAsync(sc, 0, 2 * sizeof(uint64_t), s));
-  LAUNCH("heads", k_heads, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, (uint32_t)n_ids, sc + 1);
+  if (((uintptr_t)ent & 15) == 0) {
+    LAUNCH("heads", k_heads4, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, (uint32_t)n_ids, sc + 1);
+  } else {
+    LAUNCH("heads", k_heads, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, (uint32_t)n_ids, sc + 1);
+  }
   LAUNCH("scan", k_scan_wide, dim3(1), dim3(kScanWide), s, tc, tiles, sc);
   uint64_t host[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(host, sc, sizeof(host), hipMemcpyDeviceToHost, s));

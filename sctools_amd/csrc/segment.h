@@ -50,6 +50,57 @@ __global__ void k_heads(const int32_t* __restrict__ key, int64_t n, uint64_t* __
   }
 }
 
+// k_heads with 16-byte loads: thread t of item j owns records [4(j*kBlock + t), +4) of the
+// tile; the record before its first comes from the previous lane (lane 0 loads it).  Needs a
+// 16-byte aligned column (the host checks and falls back to k_heads).
+__global__ void __launch_bounds__(kBlock) k_heads4(const int32_t* __restrict__ key, int64_t n,
+                                                   uint64_t* __restrict__ tile_cnt, uint32_t* __restrict__ seen,
+                                                   uint32_t n_ids, uint64_t* __restrict__ dup_flag) {
+  constexpr int kVec = kItems / 4;
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int lane = threadIdx.x & (kWave - 1);
+  int4 v[kVec];
+#pragma unroll
+  for (int j = 0; j < kVec; j++) {  // every load issued before any compare
+    const int64_t p = base + 4 * ((int64_t)j * kBlock + threadIdx.x);
+    if (p + 3 < n) {
+      v[j] = *reinterpret_cast<const int4*>(key + p);
+    } else {
+      v[j].x = p < n ? key[p] : 0;
+      v[j].y = p + 1 < n ? key[p + 1] : 0;
+      v[j].z = p + 2 < n ? key[p + 2] : 0;
+      v[j].w = 0;
+    }
+  }
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kVec; j++) {
+    const int64_t p = base + 4 * ((int64_t)j * kBlock + threadIdx.x);
+    int32_t prev = __shfl_up(v[j].w, 1);
+    if (lane == 0 && p > 0 && p < n) prev = key[p - 1];
+    const int32_t r[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const bool in = p + i < n;
+      const bool h = in && (p + i == 0 || r[i] != (i == 0 ? prev : r[i - 1]));
+      c += h ? 1 : 0;
+      if (h && seen) {
+        if ((uint32_t)r[i] >= n_ids) atomicOr((unsigned long long*)dup_flag, 2ull);  // id outside the dictionary
+        else if (atomicAdd(&seen[r[i]], 1u) != 0u) atomicOr((unsigned long long*)dup_flag, 1ull);
+      }
+    }
+  }
+  __shared__ uint64_t red[kWaves];
+  c = wave_sum(c);
+  if (lane == 0) red[threadIdx.x / kWave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < kWaves; w++) t += red[w];
+    tile_cnt[blockIdx.x] = t;
+  }
+}
+
 struct KeyCols {
   const int32_t* ent;  // column whose runs are the entities
   const int32_t* k1;

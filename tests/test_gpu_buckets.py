@@ -204,3 +204,25 @@ def test_ids_outside_the_dictionaries_are_rejected(eng, column):
             eng.compute(cols, "cell", dims, gm, gm, float_mode="exact")
         with pytest.raises(N.EngineError, match="outside"):
             eng.cell_and_gene(cols, dims, gm)
+
+
+@pytest.mark.parametrize("n", [1, 5, 4099, 1_000_003, 20_000_002])
+def test_run_count_aligned_and_misaligned_columns(eng, n):
+    """Entity-run counting (k_heads4 on 16-byte aligned columns, k_heads otherwise) and the
+    chunked tile-count scan (> 4096 tiles at 20M records) against numpy on the same runs."""
+    from sctools_amd import _native as N
+    from sctools_amd import engine as E
+
+    rng = np.random.default_rng(n)
+    lens = rng.geometric(1.0 / 37, size=n)
+    cell = np.repeat(np.arange(lens.size, dtype=np.int32), lens)[:n]
+    cell = (cell * 7919 % 1_000_003).astype(np.int32)  # runs of distinct, unsorted values
+    want = 1 + int(np.count_nonzero(cell[1:] != cell[:-1]))
+    dims = E.Dims(1_000_003, 1, 1)
+    for shift in (0, 1):  # shift 1: the cell column starts 4 bytes past a 16-byte boundary
+        buf = torch.zeros(n + 1, dtype=torch.int32, device=eng.device)
+        buf[shift:shift + n] = torch.from_numpy(cell).to(eng.device)
+        cols = {c: torch.zeros(n, dtype=E._TORCH_DTYPES[c], device=eng.device) for c in N.RECORD_COLUMNS}
+        cols["cell"] = buf[shift:shift + n]
+        assert (cols["cell"].data_ptr() % 16 == 0) == (shift == 0)
+        assert eng.count_entities(cols, "cell", dims) == want, shift
