@@ -76,33 +76,73 @@ __device__ __forceinline__ void wave_atomic_min(uint32_t* dst, bool on, uint32_t
 // an XF tag other than INTERGENIC (gene_col != SKIP covers "has the tag" and "no ','"); the
 // group counts when exactly one distinct name is implicated -- for a one-alignment group that
 // is the same test.
-__global__ void k_cm_groups(CountCols c, CountKey K, uint64_t* __restrict__ keys, uint32_t* __restrict__ keep,
-                            uint32_t* __restrict__ cell_first, unsigned long long* __restrict__ unknown,
-                            uint32_t* __restrict__ err) {
+//
+// One lane per record: every lane loads its own alignment (coalesced) and classifies it; a group
+// that closes inside the wave is resolved with ballots over its lanes (first implicated gene,
+// any other implicated gene, any gene id outside the dictionary).  Only a group still open at
+// the wave's last lane walks its remaining records in a loop.
+__device__ __forceinline__ void cm_classify(const CountCols& c, int64_t j, int32_t& g, bool& implicated, bool& bad) {
+  g = c.gene[j];
+  bad = (uint32_t)g >= (uint32_t)c.n_gene;
+  const uint8_t x = c.xf[j];
+  implicated = !bad && x != kXfAbsent && x != kXfIntergenic && c.gene_col[g] != -1;
+}
+
+__global__ void __launch_bounds__(kBlock) k_cm_groups(CountCols c, CountKey K, uint64_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ keep, uint32_t* __restrict__ cell_first,
+                                                      unsigned long long* __restrict__ unknown,
+                                                      uint32_t* __restrict__ err) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wbase = i - lane;
+  const bool in = i < c.n;
+  const bool head = in && (i == 0 || c.qhead[i]);
+  int32_t g = 0;
+  bool impl = false, badg = false;
+  if (in) cm_classify(c, i, g, impl, badg);
+  const uint64_t H = __ballot(head);
+  const uint64_t I = __ballot(impl);
+  const uint64_t Bm = __ballot(badg);
+  // this lane's group within the wave: lanes [hd, nx)
+  const uint64_t upto = lane == kWave - 1 ? ~0ull : ((2ull << lane) - 1);
+  const uint64_t hbelow = H & upto;
+  const int hd = hbelow ? 63 - __clzll((long long)hbelow) : -1;
+  const uint64_t habove = H & ~upto;
+  const int nx = habove ? __ffsll((unsigned long long)habove) - 1 : kWave;
+  const uint64_t seg = hd < 0 ? 0ull : ((nx == kWave ? ~0ull : ((1ull << nx) - 1)) & ~((1ull << hd) - 1));
+  const uint64_t Iseg = I & seg;
+  const int first = Iseg ? __ffsll((unsigned long long)Iseg) - 1 : lane;
+  const int32_t sel_w = __shfl(g, first);
+  const uint64_t D = __ballot(impl && hd >= 0 && g != sel_w);
   bool kept = false;
   int32_t cell = 0;
-  if (i < c.n && (c.qhead[i] || i == 0)) {
+  if (head) {
     cell = c.cell[i];
     const int32_t umi = c.umi[i];
     if ((uint32_t)cell >= (uint32_t)c.n_cell || (uint32_t)umi >= (uint32_t)c.n_umi) {
       atomicOr(err, 1u);
     } else if (cell != c.cell_none && umi != c.umi_none) {
-      int32_t sel = -1;
-      bool multi = false;
-      for (int64_t j = i; j < c.n && (j == i || !c.qhead[j]); j++) {
-        const int32_t g = c.gene[j];
-        if ((uint32_t)g >= (uint32_t)c.n_gene) {
-          atomicOr(err, 1u);
-          sel = -1;
-          break;
+      int32_t sel = Iseg ? sel_w : -1;
+      bool multi = (D & seg) != 0;
+      bool bad = (Bm & seg) != 0;
+      const int64_t past = wbase + kWave;  // the group may continue past the wave's last lane
+      if (!bad && nx == kWave && past < c.n && !c.qhead[past]) {
+        for (int64_t j = past; j < c.n && !c.qhead[j]; j++) {
+          int32_t gj;
+          bool ij, bj;
+          cm_classify(c, j, gj, ij, bj);
+          if (bj) {
+            bad = true;
+            break;
+          }
+          if (!ij) continue;
+          if (sel < 0) sel = gj;
+          else if (gj != sel) multi = true;
         }
-        const uint8_t x = c.xf[j];
-        if (x == kXfAbsent || x == kXfIntergenic || c.gene_col[g] == -1) continue;
-        if (sel < 0) sel = g;
-        else if (g != sel) multi = true;
       }
-      if (sel >= 0 && !multi) {
+      if (bad) {
+        atomicOr(err, 1u);
+      } else if (sel >= 0 && !multi) {
         int32_t col = c.gene_col[sel];
         if (col < 0 || col >= c.n_cols) {  // the reference's gene_name_to_index[gene_name] KeyError
           atomicMin(unknown, (unsigned long long)i);
@@ -113,7 +153,7 @@ __global__ void k_cm_groups(CountCols c, CountKey K, uint64_t* __restrict__ keys
       }
     }
   }
-  if (i < c.n) keep[i] = kept ? 1u : 0u;
+  if (in) keep[i] = kept ? 1u : 0u;
   wave_atomic_min(cell_first, kept, (uint32_t)cell, (uint32_t)i);
 }
 

@@ -82,9 +82,11 @@ def gpu_count(eng, arrays, cells, umis, genes, names):
     return [t.cpu().numpy() for t in res]
 
 
-@pytest.mark.parametrize("n,seed", [(300_000, 1), (1_000_000, 2)])
-def test_count_matrix_matches_column_oracle(eng, n, seed):
-    arrays, cells, umis, genes, names = synthetic_columns(n, seed)
+@pytest.mark.parametrize("n,seed,group_p", [(300_000, 1, 0.3), (1_000_000, 2, 0.3), (200_000, 5, 0.97)])
+def test_count_matrix_matches_column_oracle(eng, n, seed, group_p):
+    """group_p 0.97: query-name groups of ~33 alignments, many spanning wave boundaries (the
+    count-groups kernel resolves in-wave groups by ballots and walks the rest)."""
+    arrays, cells, umis, genes, names = synthetic_columns(n, seed, group_p=group_p)
     row_cell, indptr, indices, data = gpu_count(eng, arrays, cells, umis, genes, names)
     csr, row_index, _ = O.count_columns(arrays, cells, umis, genes, names)
     assert np.array_equal(indptr, csr.indptr) and np.array_equal(indices, csr.indices)
@@ -132,3 +134,26 @@ def test_count_matrix_rejects_keys_wider_than_63_bits(eng):
     cols = [torch.from_numpy(bad[c]).to(dev) for c in ("cell", "umi", "gene", "xf", "qhead")]
     with pytest.raises(N.EngineError, match="outside"):
         eng.count_matrix(*cols, gc, len(cells), len(umis), 0, 0, len(names))
+
+
+def test_count_matrix_gene_id_outside_dictionary_in_a_group_tail(eng):
+    """A gene id outside the dictionary on a non-first alignment of a counted group is rejected,
+    also when the group continues past a wave of 64 lanes; in a group whose first alignment has
+    no cell barcode it is never looked at (the reference skips the group before its genes)."""
+    from sctools_amd import _native as N
+
+    arrays, cells, umis, genes, names = synthetic_columns(4096, 6, group_p=0.0)
+    dev = eng.device
+    gc = torch.from_numpy(C.gene_columns(genes, names)).to(dev)
+    for start, length, bad_at in ((100, 5, 103), (60, 10, 68), (30, 200, 220)):
+        a = {k: v.copy() for k, v in arrays.items()}
+        a["qhead"][start + 1:start + length] = 0
+        a["cell"][start], a["umi"][start] = 7, 9
+        a["gene"][bad_at] = len(genes) + 3
+        cols = [torch.from_numpy(a[c]).to(dev) for c in ("cell", "umi", "gene", "xf", "qhead")]
+        with pytest.raises(N.EngineError, match="outside"):
+            eng.count_matrix(*cols, gc, len(cells), len(umis), 0, 0, len(names))
+        a["cell"][start] = 0  # cell None: the group is skipped, its genes unread
+        cols = [torch.from_numpy(a[c]).to(dev) for c in ("cell", "umi", "gene", "xf", "qhead")]
+        res, unknown = eng.count_matrix(*cols, gc, len(cells), len(umis), 0, 0, len(names))
+        assert unknown == -1
