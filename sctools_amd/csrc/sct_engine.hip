@@ -157,8 +157,7 @@ int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool du
   }
   LAUNCH("scan", k_scan_wide, dim3(1), dim3(kScanWide), s, tc, tiles, sc);
   uint64_t host[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(host, sc, sizeof(host), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  if (int rb = readback(host, sc, sizeof(host), s)) return rb;
   *n_ent = (int64_t)host[0];
   if (dup) *dup = host[1] & 1;
   if (host[1] & 2) return fail(SCT_EINVAL, "an entity id lies outside [0, %d)", n_ids);
@@ -210,8 +209,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   LAUNCH("bucket_level0", k_bucket_level0, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, ent_start, n_ent, n,
          bdesc, bent, seg[0], work[0], bigs, ctl);
   BucketCtl h{};
-  HIPCHK(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  if (int rb = readback(&h, ctl, sizeof(h), s)) return rb;
   if (h.err & 2) return fail(SCT_EINVAL, "a gene / cell / umi id lies outside its dictionary size");
   if (h.err) return 1;
   int depth = 0, level = 1, c = 0;
@@ -235,8 +233,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
            work[c ^ 1], giants, bigs, ctl);
     LAUNCH("bucket_scatter", k_bucket_scatter, dim3(h.n_work), dim3(kBlock), s, kin, vin, kout, vout,
            (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
-    HIPCHK(hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if (int rb = readback(&h, ctl, sizeof(h), s)) return rb;
     c ^= 1;
     depth += bits;
     level++;
@@ -391,8 +388,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
                                                    ent_start, partials, gcounts, L.n_buckets, &ctl->err);
     if (rc) return rc;
     uint32_t err = 0;  // the bucket path reads the flag at its first level sync
-    HIPCHK(hipMemcpyAsync(&err, &ctl->err, sizeof(err), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if (int rb = readback(&err, &ctl->err, sizeof(err), s)) return rb;
     if (err & 2) return fail(SCT_EINVAL, "a gene / cell / umi id lies outside its dictionary size");
   }
   if (rc) return rc;
@@ -801,8 +797,7 @@ int sct_verify_sort(const sct_plan_t* plan, const sct_records_t* rec, const int3
   LAUNCH("tag_verify", k_verify_order, dim3((unsigned)cdiv(rec->n - 1, kBlock)), dim3(kBlock), s, *rec, tiebreak,
          f[0], f[1], f[2], nf, bad);
   unsigned long long h = 0;
-  HIPCHK(hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  if (int rb = readback(&h, bad, sizeof(h), s)) return rb;
   *first_violation = h >= none ? -1 : (int64_t)h;
   return SCT_OK;
 }
@@ -875,8 +870,7 @@ int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void*
   LAUNCH("count_compact", k_cm_compact, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), s, (const uint64_t*)B.kb,
          (const uint32_t*)fa, (const uint32_t*)oa, n, B.ka, B.va, sc + 1);
   uint64_t h[6];
-  HIPCHK(hipMemcpyAsync(h, sc, sizeof(h), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  if (int rb = readback(h, sc, sizeof(h), s)) return rb;
   if (h[5]) return fail(SCT_EINVAL, "a dictionary id is outside its dictionary");
   if (h[0] != ~0ull) {
     out->unknown_record = (int64_t)h[0];
@@ -902,8 +896,7 @@ int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void*
     // 3. row order: counted cells by the record index of their first counted molecule
     LAUNCH("count_rowkeys", k_cm_rowkeys, dim3((unsigned)cdiv(nc, kBlock)), dim3(kBlock), s,
            (const uint32_t*)cell_first, (int32_t)nc, B.ka, B.va, sc + 4);
-    HIPCHK(hipMemcpyAsync(h, sc, sizeof(h), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if (int rb = readback(h, sc, sizeof(h), s)) return rb;
     nnz = (int64_t)h[2];
     n_triples = h[3];
     n_rows = (int64_t)h[4];

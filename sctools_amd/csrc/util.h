@@ -4,6 +4,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <string.h>
 
 #include <string>
 #include <utility>
@@ -42,6 +43,20 @@ inline int fail(int code, const char* fmt, ...) {
   } while (0)
 
 #define LAUNCHCHK() HIPCHK(hipGetLastError())
+
+// Small device -> host readbacks (run counts, level counters, error flags) between launches:
+// copied through a pinned per-thread buffer, since a copy into pageable memory is staged by
+// the runtime; then the stream is synchronized.
+inline int readback(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  constexpr size_t kCap = 256;
+  static thread_local void* buf = nullptr;
+  if (bytes > kCap) return fail(SCT_EINVAL, "readback of %zu bytes exceeds %zu", bytes, kCap);
+  if (!buf) HIPCHK(hipHostMalloc(&buf, kCap, hipHostMallocPortable));
+  HIPCHK(hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  memcpy(dst, buf, bytes);
+  return SCT_OK;
+}
 
 // ---------------- host: optional per-kernel timing with HIP events ----------------
 struct ProfEntry {
