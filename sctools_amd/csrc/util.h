@@ -47,14 +47,22 @@ inline int fail(int code, const char* fmt, ...) {
 // Small device -> host readbacks (run counts, level counters, error flags) between launches:
 // copied through a pinned per-thread buffer, since a copy into pageable memory is staged by
 // the runtime; then the stream is synchronized.
+// The buffer belongs to the calling host thread and is freed when the thread exits.
+struct PinnedReadback {
+  static constexpr size_t kCap = 256;
+  void* buf = nullptr;
+  ~PinnedReadback() {
+    if (buf) (void)hipHostFree(buf);
+  }
+};
 inline int readback(void* dst, const void* src, size_t bytes, hipStream_t s) {
-  constexpr size_t kCap = 256;
-  static thread_local void* buf = nullptr;
-  if (bytes > kCap) return fail(SCT_EINVAL, "readback of %zu bytes exceeds %zu", bytes, kCap);
-  if (!buf) HIPCHK(hipHostMalloc(&buf, kCap, hipHostMallocPortable));
-  HIPCHK(hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToHost, s));
+  static thread_local PinnedReadback rb;
+  if (bytes > PinnedReadback::kCap)
+    return fail(SCT_EINVAL, "readback of %zu bytes exceeds %zu", bytes, PinnedReadback::kCap);
+  if (!rb.buf) HIPCHK(hipHostMalloc(&rb.buf, PinnedReadback::kCap, hipHostMallocPortable));
+  HIPCHK(hipMemcpyAsync(rb.buf, src, bytes, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  memcpy(dst, buf, bytes);
+  memcpy(dst, rb.buf, bytes);
   return SCT_OK;
 }
 

@@ -52,6 +52,11 @@ class MergeGeneMetrics(MergeMetrics):
     @staticmethod
     def _merge_pair(nucleus: pd.DataFrame, leaf: pd.DataFrame) -> pd.DataFrame:
         both = pd.concat([nucleus, leaf], axis=0)
+        # the gatherer writes a ``None`` row for reads without GE; read_csv makes its index NaN
+        # and the reference's groupby(level=0) drops such rows (merge.py:176, dropna default)
+        both = both[both.index.notna()]
+        if both.shape[0] == 0:
+            raise ValueError("no gene rows left to merge: every row has a missing (None) gene index")
         grouped = both.groupby(level=0)
         summed = grouped.agg({c: "sum" for c in _SUM_COLUMNS})
         weights = both["n_reads"].to_numpy(dtype=np.float64)
@@ -59,6 +64,8 @@ class MergeGeneMetrics(MergeMetrics):
         codes = grouped.ngroup().to_numpy()
         n_groups = summed.shape[0]
         wsum = np.bincount(codes, weights=weights, minlength=n_groups)
+        if (wsum == 0).any():  # np.average raises on zero weights (merge.py:108-138)
+            raise ZeroDivisionError("Weights sum to zero, can't be normalized")
         for c in _AVERAGE_COLUMNS:
             vals = both[c].to_numpy(dtype=np.float64)
             # np.average(x, weights=n_reads) per group; NaN propagates like the reference

@@ -20,7 +20,11 @@ Distributions:
   NH == 1 for 90 %, 5 % spliced;
 * read length 98, 13 % soft-clipped by 1-29 bases; CY 16, UY 10; binned
   Phred values with the measured per-bin weights of ``small-cell-sorted.bam``;
-* CR != CB for 1 %, UR != UB for 0.2 %.
+* CR != CB for 1 %, UR != UB for 0.2 %;
+* config 5 (``p_secondary`` > 0): a record may be a secondary alignment of the record before it
+  in its molecule: same query name, cell barcode and UMI, another reference, both NH > 1.
+  ``extra["qname"]`` holds every record's query-name rank (names "Q%010d" of the primary's
+  ordinal, so the rank is that ordinal) and ``extra["n_qnames"]`` their number.
 """
 
 from dataclasses import dataclass, field
@@ -58,6 +62,7 @@ class SynthConfig:
     p_bad_cb: float = 0.01
     p_bad_ub: float = 0.002
     p_none_cell_reads: float = 0.0  # fraction of reads emitted as a leading CB=None run
+    p_secondary: float = 0.0  # records that are a secondary alignment of the previous read (config 5)
     keep_qualities: bool = False  # keep per-base aligned qualities (fixtures only)
 
 
@@ -201,6 +206,16 @@ def generate(cfg: SynthConfig, device="cpu", chunk: int = 8_000_000) -> SynthDat
     umi = mol_umi[mol_id].to(torch.int32)
     ref = mol_ref[mol_id].to(torch.int32)
     pos = (mol_anchor[mol_id] + 50 * torch.randint(0, 4, (n,), generator=gen, device=dev)).to(torch.int32)
+    # secondary alignments: a non-head record of a molecule may repeat the previous record's read
+    # (same query name, CB, UB) at another locus; both then have NH > 1
+    qname = None
+    secondary = None
+    if cfg.p_secondary > 0:
+        secondary = (torch.rand(n, generator=gen, device=dev) < cfg.p_secondary) & ~mol_head
+        qname = (torch.cumsum((~secondary).to(torch.int64), 0) - 1).to(torch.int32)
+        shift = torch.randint(1, 25, (n,), generator=gen, device=dev, dtype=torch.int64)
+        ref = torch.where(secondary, ((ref.to(torch.int64) + shift) % 25).to(torch.int32), ref)
+        del shift
     del mol_id, mol_head, mu, grank, gsel
 
     def bern(prob):
@@ -211,6 +226,11 @@ def generate(cfg: SynthConfig, device="cpu", chunk: int = 8_000_000) -> SynthDat
     dup = bern(cfg.p_dup) & ~unmapped
     spliced = bern(cfg.p_spliced) & ~unmapped
     nh1 = bern(cfg.p_nh1)
+    if secondary is not None:  # a multi-mapped read: the primary and its secondaries have NH > 1
+        multi = secondary.clone()
+        multi[:-1] |= secondary[1:]
+        nh1 &= ~multi
+        del multi
     perfect_umi = ~bern(cfg.p_bad_ub)
     has_cb = (cell != 0) if has_none else torch.ones(n, dtype=torch.bool, device=dev)
     perfect_cb = has_cb & ~bern(cfg.p_bad_cb)
@@ -286,7 +306,8 @@ def generate(cfg: SynthConfig, device="cpu", chunk: int = 8_000_000) -> SynthDat
         gene_is_multi=gene_is_multi,
         cell_has_none=has_none,
         quals=quals,
-        extra={"per_cell": per_cell.numpy(), "n_none": n_none},
+        extra={"per_cell": per_cell.numpy(), "n_none": n_none, "qname": qname,
+               "n_qnames": int(qname[-1].item()) + 1 if qname is not None else 0},
     )
 
 

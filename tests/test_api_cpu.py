@@ -31,6 +31,33 @@ def test_merges_match_reference(tmp_path, kind, merger):
     np.testing.assert_allclose(got.to_numpy(dtype=float), want.to_numpy(dtype=float), rtol=1e-9, equal_nan=True)
 
 
+def test_gene_merge_drops_none_rows_like_reference(tmp_path):
+    """Gene CSVs carry a `None` row for reads without GE; the reference's groupby drops it
+    (fixture: tests/golden/make_merge_none.py), and raises when no row is left."""
+    none = os.path.join(H.GOLDEN, "ref", "cell-sorted-missing-cb.gene.csv")
+    small = os.path.join(H.GOLDEN, "ref", "small-gene-sorted.gene.csv")
+    out = str(tmp_path / "m")
+    MergeGeneMetrics([none, small, none], out).execute()
+    got = _read(out + ".csv.gz")
+    want = _read(os.path.join(MERGE, "gene_none_merged.csv"))
+    assert list(got.columns) == list(want.columns)
+    assert list(got.index) == list(want.index)
+    np.testing.assert_allclose(got.to_numpy(dtype=float), want.to_numpy(dtype=float), rtol=1e-9, equal_nan=True)
+    with pytest.raises(ValueError):
+        MergeGeneMetrics([none, none], str(tmp_path / "n")).execute()
+
+
+def test_gene_merge_zero_weights_raise(tmp_path):
+    """np.average(..., weights=n_reads) raises ZeroDivisionError when a gene's weights sum to 0."""
+    src = os.path.join(MERGE, "gene_part1.csv")
+    df = _read(src)
+    df["n_reads"] = 0
+    p = str(tmp_path / "z.csv")
+    df.to_csv(p)
+    with pytest.raises(ZeroDivisionError):
+        MergeGeneMetrics([p, p], str(tmp_path / "zz")).execute()
+
+
 def test_header_from_aggregators():
     assert R.header_line("cell").rstrip("\n") == H.golden_text("small-cell-sorted", "cell").split("\n")[0]
     assert R.header_line("gene").rstrip("\n") == H.golden_text("small-gene-sorted", "gene").split("\n")[0]
