@@ -11,7 +11,7 @@ CSVFMT := sctools_amd/libsct_csv.so
 all: $(ENGINE) $(BAMDEC) $(CSVFMT) oracle/liboracle.so tests/native/libfxcheck.so
 
 $(ENGINE): $(SRC) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC)
+	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC) -L/opt/rocm/lib -lrccl
 
 $(BAMDEC): sctools_amd/csrc/bamdec.cpp include/sct_bam.h
 	g++ -O3 -std=c++17 -fopenmp -fPIC -shared -Wall -o $@ sctools_amd/csrc/bamdec.cpp -lz

@@ -214,6 +214,27 @@ int sct_cell_metrics_gene_partials(const sct_plan_t* plan, const sct_records_t* 
 int sct_finalize_partials(int32_t mode, const int64_t* partials, int64_t rows, int64_t* out_ints,
                           double* out_floats, void* stream);
 
+/* ---- multi-GPU: the gene-partial all-reduce ----
+ * Replaces MergeGeneMetrics' CSV merge of cell-disjoint chunks (merge.py:74-191; the
+ * chunks come from SplitBam, bam.py:361-488).  Each rank holds [rows][SCT_NP] int64
+ * partial rows of its cell shard (sct_gene_partials / sct_cell_metrics_gene_partials);
+ * their lanes are plain integer sums, so one in-place sum all-reduce over RCCL (xGMI)
+ * gives every rank the rows of the union of the shards, bit for bit, in any rank order;
+ * sct_finalize_partials then yields the unsharded gene rows.
+ * `comm` is an ncclComm_t (RCCL) passed as void*: from the helpers below or from the
+ * caller's own RCCL setup.  Does not synchronize `stream`. */
+int sct_allreduce_gene_partials(int64_t* partials, int64_t rows, void* comm, void* stream);
+
+/* Communicator helpers for callers without their own RCCL setup.
+ * One process, several devices: sct_comm_init_all fills comms[0..ndev) (ncclCommInitAll);
+ * drive each from its own host thread (or one thread with group calls).
+ * One process per device: rank 0 calls sct_comm_unique_id (id: >= 128 bytes, host), the id
+ * travels out of band, then every rank calls sct_comm_init_rank on its device. */
+int sct_comm_unique_id(uint8_t* id, size_t bytes);
+int sct_comm_init_rank(void** comm, int nranks, const uint8_t* id, size_t bytes, int rank, int device);
+int sct_comm_init_all(void** comms, int ndev, const int* devices);
+int sct_comm_destroy(void* comm);
+
 /* ---- tag sort (TagSortBam / bam.sort_by_tags_and_queryname, bam.py:638-709;
  *      platform.py:55-104) ---- */
 #define SCT_ORDER_CELL 0          /* CB only: what cell metrics need (input order kept within a cell) */

@@ -35,7 +35,9 @@ RECORD_COLUMNS = ("cell", "umi", "gene", "ref", "pos", "gq_sum", "gq_len", "gq_g
 EXPORTED = ("sct_abi_version", "sct_last_error", "sct_workspace_size", "sct_count_entities",
             "sct_compute_metrics", "sct_gene_partials", "sct_cell_metrics_gene_partials",
             "sct_finalize_partials", "sct_profile_enable", "sct_profile_only", "sct_profile_read",
-            "sct_tag_sort_workspace_size", "sct_tag_sort", "sct_verify_sort", "sct_count_matrix_workspace_size", "sct_count_matrix")
+            "sct_tag_sort_workspace_size", "sct_tag_sort", "sct_verify_sort", "sct_count_matrix_workspace_size", "sct_count_matrix",
+            "sct_allreduce_gene_partials", "sct_comm_unique_id", "sct_comm_init_rank", "sct_comm_init_all",
+            "sct_comm_destroy")
 ORDER_CELL, ORDER_CELL_UMI_GENE, ORDER_GENE_CELL_UMI = 0, 1, 2
 PLAN_GENE_PARTIALS = 0x1
 
@@ -140,6 +142,16 @@ def load() -> ctypes.CDLL:
     L.sct_count_matrix_workspace_size.argtypes = [ctypes.POINTER(CountInput), ctypes.POINTER(ctypes.c_size_t)]
     L.sct_count_matrix.restype = ctypes.c_int
     L.sct_count_matrix.argtypes = [ctypes.POINTER(CountInput), ctypes.POINTER(CountOutput), vp, ctypes.c_size_t, vp]
+    L.sct_allreduce_gene_partials.restype = ctypes.c_int
+    L.sct_allreduce_gene_partials.argtypes = [vp, i64, vp, vp]
+    L.sct_comm_unique_id.restype = ctypes.c_int
+    L.sct_comm_unique_id.argtypes = [vp, ctypes.c_size_t]
+    L.sct_comm_init_rank.restype = ctypes.c_int
+    L.sct_comm_init_rank.argtypes = [ctypes.POINTER(vp), ctypes.c_int, vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+    L.sct_comm_init_all.restype = ctypes.c_int
+    L.sct_comm_init_all.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.sct_comm_destroy.restype = ctypes.c_int
+    L.sct_comm_destroy.argtypes = [vp]
     L.sct_profile_enable.restype = ctypes.c_int
     L.sct_profile_enable.argtypes = [ctypes.c_int]
     L.sct_profile_only.restype = ctypes.c_int

@@ -17,13 +17,15 @@
 //   gene.h      gene buckets -> per-gene partial rows (LDS bins)
 //   finalize.h  partial rows -> output rows; sequential Welford float path
 //   tagsort.h   TagSortBam orders on the device; countmat.h  CountMatrix (CSR)
+//   comm.h      RCCL all-reduce of gene partials (replaces MergeGeneMetrics, merge.py:74-191)
 //
-// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared.
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared ... -lrccl.
 // -ffp-contract=off keeps every Welford operation separately rounded, as Python does.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include "comm.h"
 #include "common.h"
 #include "countmat.h"
 #include "finalize.h"

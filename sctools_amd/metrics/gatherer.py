@@ -15,6 +15,13 @@ in one launch sequence.  ``float_mode='welford'`` (default) reproduces the
 reference's sequential Welford floats bit for bit; ``'exact'`` computes
 correctly rounded mean / variance from exact sums (order independent,
 within 1e-12 of Welford).
+
+``devices=N`` (optional) spreads the entity runs over N GPUs, one host thread each
+(``sctools_amd.multigpu``): same rows, same order.  ``GatherCellAndGeneMetrics`` (new) writes
+the cell rows of a cell-sorted file and, from the same pass, its gene rows as TagSortBam by
+(GE, CB, UB) + ``GatherGeneMetrics`` would give them -- the SplitBam + per-chunk metrics +
+``MergeGeneMetrics`` workflow in one call, the gene partials of the devices' cell ranges summed
+by an RCCL all-reduce.
 """
 
 from typing import Optional, Set
@@ -29,11 +36,16 @@ from sctools_amd.metrics.writer import MetricCSVWriter
 
 
 def compute_rows(cols: columnar.Columns, mode: str, mitochondrial_gene_ids=frozenset(),
-                 float_mode: str = "welford", device=None):
+                 float_mode: str = "welford", device=None, devices=None):
     """Run the engine on host columns; returns (ints, floats) numpy rows of every entity run."""
     import torch
 
     from sctools_amd import engine as E
+
+    if devices is not None:
+        from sctools_amd import multigpu
+
+        return multigpu.compute_rows(cols, mode, mitochondrial_gene_ids, float_mode, devices)
 
     eng = E.get_engine(device)
     dev_cols = E.to_device(cols.arrays, eng.device)
@@ -58,13 +70,15 @@ class MetricGatherer:
     """Gathers metrics from an experiment (``gatherer.py:38-86``)."""
 
     def __init__(self, bam_file: str, output_stem: str, mitochondrial_gene_ids: Set[str] = set(),
-                 compress: bool = True, float_mode: str = "welford", device: Optional[str] = None):
+                 compress: bool = True, float_mode: str = "welford", device: Optional[str] = None,
+                 devices=None):
         self._bam_file = bam_file
         self._output_stem = output_stem
         self._compress = compress
         self._mitochondrial_gene_ids = mitochondrial_gene_ids
         self._float_mode = float_mode
         self._device = device
+        self._devices = devices  # None: one device (`device`); int N or device list: multigpu
 
     @property
     def bam_file(self) -> str:
@@ -83,7 +97,7 @@ class GatherCellMetrics(MetricGatherer):
             out.write_header(vars(CellMetrics()))
             cols = columnar.columnarize(self.bam_file, mode, columnar.MODE_CELL)
             ints, floats = compute_rows(cols, "cell", self._mitochondrial_gene_ids, self._float_mode,
-                                        self._device)
+                                        self._device, self._devices)
             write_rows(out, "cell", cols, ints, floats)
 
 
@@ -94,5 +108,45 @@ class GatherGeneMetrics(MetricGatherer):
         with MetricCSVWriter(self._output_stem, self._compress) as out:
             out.write_header(vars(GeneMetrics()))
             cols = columnar.columnarize(self.bam_file, mode, columnar.MODE_GENE)
-            ints, floats = compute_rows(cols, "gene", frozenset(), self._float_mode, self._device)
+            ints, floats = compute_rows(cols, "gene", frozenset(), self._float_mode, self._device,
+                                        self._devices)
             write_rows(out, "gene", cols, ints, floats)
+
+
+def write_grouped_gene_rows(writer: MetricCSVWriter, cols: columnar.Columns, ints: np.ndarray,
+                            floats: np.ndarray) -> None:
+    """Gene rows indexed by gene id: ids with reads, multi-gene values skipped, in id order (the
+    sorted order of the gene strings, None first -- TagSortBam's order, bam.py:698-709)."""
+    names = [cols.genes.names[g] for g in ints[:, N.I_ENTITY]]
+    keep, kept = R.select_rows("gene_grouped", ints, names)
+    writer.write_bytes(R.format_rows_bytes("gene", kept, ints[keep], floats[keep]))
+
+
+class GatherCellAndGeneMetrics(MetricGatherer):
+    """Cell rows AND gene rows of one cell-sorted BAM, from one decode and one device pass.
+
+    Cell rows: as ``GatherCellMetrics``.  Gene rows: every record of a gene id aggregated
+    together, as ``GatherGeneMetrics`` reports them for the same records re-sorted by
+    (GE, CB, UB) (TagSortBam), with exact-sum floats (within 1e-12 of Welford); it replaces
+    SplitBam + per-chunk ``CalculateGeneMetrics`` + ``MergeGeneMetrics`` (merge.py:74-191) with
+    an exact RCCL all-reduce of per-gene partials when ``devices`` > 1.
+    """
+
+    def __init__(self, bam_file: str, output_stem: str, gene_output_stem: str,
+                 mitochondrial_gene_ids: Set[str] = set(), compress: bool = True, float_mode: str = "welford",
+                 devices=1):
+        super().__init__(bam_file, output_stem, mitochondrial_gene_ids, compress, float_mode, None, devices)
+        self._gene_output_stem = gene_output_stem
+
+    def extract_metrics(self, mode: str = "rb") -> None:
+        from sctools_amd import multigpu
+
+        cols = columnar.columnarize(self.bam_file, mode, columnar.MODE_CELL)
+        (ci, cf), (gi, gf) = multigpu.compute_cell_and_gene_rows(cols, self._mitochondrial_gene_ids,
+                                                                 self._float_mode, self._devices)
+        with MetricCSVWriter(self._output_stem, self._compress) as out:
+            out.write_header(vars(CellMetrics()))
+            write_rows(out, "cell", cols, ci, cf)
+        with MetricCSVWriter(self._gene_output_stem, self._compress) as out:
+            out.write_header(vars(GeneMetrics()))
+            write_grouped_gene_rows(out, cols, gi, gf)

@@ -1,0 +1,207 @@
+"""
+Several GPUs behind the ``sctools.metrics`` drop-in: one host thread per device.
+
+The reference scales the metric path by splitting a BAM into cell-disjoint chunks
+(``SplitBam``, ``/root/reference/src/sctools/bam.py:361-488``; CLI ``platform.py:153-223``),
+running ``Calculate*Metrics`` on each chunk and merging the CSVs (``MergeCellMetrics``
+concatenates, ``MergeGeneMetrics`` folds, ``metrics/merge.py:59-191``).  Here the file is
+decoded once on the host -- so the cell / gene / umi dictionaries are global -- and:
+
+* RUN-mode rows (``GatherCellMetrics`` on a cell-sorted file, ``GatherGeneMetrics`` on a
+  gene-sorted one): the records are cut at entity-run boundaries into contiguous ranges
+  balanced by record count (``distributed.shard_bounds``); each device computes the rows of
+  its range; rows are concatenated in range order, which is file order.  No collective is
+  needed: an entity never spans two ranges.
+* Gene rows of a cell-sorted file (what ``TagSortBam`` by (GE, CB, UB) followed by
+  ``GatherGeneMetrics`` gives, or SplitBam + per-chunk gene metrics + ``MergeGeneMetrics``):
+  each device turns its cell range into additive per-gene partial rows, ONE in-place
+  RCCL all-reduce over xGMI (``sct_allreduce_gene_partials`` on communicators from
+  ``sct_comm_init_all``) sums them, and the finalize kernel turns the sum into gene rows --
+  exactly the rows of the unsharded file (exact-sum floats).
+
+The threads only issue work: H2D copies, C-ABI calls and the collective all release the GIL.
+"""
+
+import ctypes
+import threading
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from sctools_amd import _native as N
+from sctools_amd import columnar
+from sctools_amd import distributed as D
+
+
+def parse_devices(devices) -> List[int]:
+    """``devices``: an int N (devices 0..N-1) or a sequence of device indices."""
+    if isinstance(devices, int):
+        if devices < 1:
+            raise ValueError("devices must be >= 1")
+        return list(range(devices))
+    out = [int(d) for d in devices]
+    if not out or len(set(out)) != len(out):
+        raise ValueError("devices must be distinct device indices")
+    return out
+
+
+class DeviceGroup:
+    """Engines on several devices, one worker thread per device, RCCL communicators on demand."""
+
+    def __init__(self, devices):
+        from sctools_amd import engine as E
+
+        self.devices = parse_devices(devices)
+        if not torch.cuda.is_available():
+            raise RuntimeError("sctools_amd needs ROCm GPUs; there is no CPU fallback")
+        if max(self.devices) >= torch.cuda.device_count():
+            raise ValueError("device %d requested, %d visible" % (max(self.devices), torch.cuda.device_count()))
+        self.engines = [E.get_engine(torch.device("cuda", d)) for d in self.devices]
+        self.lib = N.load()
+        self._comms: Optional[ctypes.Array] = None
+
+    @property
+    def size(self) -> int:
+        return len(self.devices)
+
+    def run(self, fn: Callable[[int], object]) -> List[object]:
+        """fn(rank) on every rank, each in its own thread with its device current."""
+        out: List[object] = [None] * self.size
+        errs: List[Optional[BaseException]] = [None] * self.size
+
+        def work(r):
+            try:
+                with torch.cuda.device(self.devices[r]):
+                    out[r] = fn(r)
+            except BaseException as e:  # re-raised on the caller's thread
+                errs[r] = e
+
+        threads = [threading.Thread(target=work, args=(r,)) for r in range(self.size)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        for e in errs:
+            if e is not None:
+                raise e
+        return out
+
+    def comms(self) -> ctypes.Array:
+        """The group's communicators (ncclCommInitAll); create them on the caller's thread before
+        the ranks' threads use them."""
+        if self._comms is None:
+            comms = (ctypes.c_void_p * self.size)()
+            devs = (ctypes.c_int * self.size)(*self.devices)
+            N.check(self.lib.sct_comm_init_all(comms, self.size, devs))
+            self._comms = comms
+        return self._comms
+
+    def allreduce_partials(self, rank: int, partials: torch.Tensor) -> None:
+        """In-place sum of every rank's [rows, SCT_NP] int64 partials (call from every rank's thread)."""
+        if partials.dtype != torch.int64 or not partials.is_contiguous():
+            raise TypeError("partials must be contiguous int64")
+        stream = ctypes.c_void_p(torch.cuda.current_stream(partials.device).cuda_stream)
+        N.check(self.lib.sct_allreduce_gene_partials(ctypes.c_void_p(partials.data_ptr()), int(partials.shape[0]),
+                                                     ctypes.c_void_p(self.comms()[rank]), stream))
+
+    def close(self) -> None:
+        if self._comms is not None:
+            for c in self._comms:
+                self.lib.sct_comm_destroy(ctypes.c_void_p(c))
+            self._comms = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def _shard_arrays(arrays, lo, hi):
+    return {c: np.ascontiguousarray(a[lo:hi]) for c, a in arrays.items()}
+
+
+def _dims(cols: columnar.Columns):
+    from sctools_amd import engine as E
+
+    return E.Dims(len(cols.cells), len(cols.genes), len(cols.umis))
+
+
+def compute_rows(cols: columnar.Columns, mode: str, mitochondrial_gene_ids=frozenset(), float_mode: str = "welford",
+                 devices=1) -> Tuple[np.ndarray, np.ndarray]:
+    """RUN-mode rows of every entity run, the runs spread over ``devices``; the same rows, in the
+    same order, as one device computes (``metrics.gatherer.compute_rows``)."""
+    from sctools_amd import engine as E
+
+    key = cols.arrays["cell" if mode == "cell" else "gene"]
+    mito, multi = cols.gene_flags(mitochondrial_gene_ids)
+    dims = _dims(cols)
+    with DeviceGroup(devices) as g:
+        bounds = D.shard_bounds(key, g.size)
+
+        def rank_rows(r):
+            lo, hi = bounds[r]
+            if hi == lo:
+                return np.zeros((0, N.SCT_NI), np.int64), np.zeros((0, N.SCT_NF), np.float64)
+            eng = g.engines[r]
+            dev_cols = E.to_device(_shard_arrays(cols.arrays, lo, hi), eng.device)
+            gm = torch.from_numpy(mito).to(eng.device)
+            gx = torch.from_numpy(multi).to(eng.device)
+            ints, floats = eng.compute(dev_cols, mode, dims, gm, gx, float_mode=float_mode)
+            ints, floats = ints.cpu().numpy(), floats.cpu().numpy()
+            ints[:, N.I_ENTITY] += lo  # first-record index in the whole file
+            return ints, floats
+
+        parts = g.run(rank_rows)
+    return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+
+
+def compute_cell_and_gene_rows(cols: columnar.Columns, mitochondrial_gene_ids=frozenset(),
+                               float_mode: str = "exact", devices=1):
+    """Cell rows of a cell-sorted record set and its grouped gene rows (every record of a gene
+    id, as after TagSortBam by (GE, CB, UB)), cell ranges spread over ``devices``, gene partials
+    summed by the RCCL all-reduce.  Returns ((cell ints, cell floats), (gene ints, gene floats));
+    gene rows are indexed by gene id (zero-read ids included; the writer skips them)."""
+    from sctools_amd import engine as E
+
+    cell = cols.arrays["cell"]
+    if cell.shape[0]:  # grouped gene rows need every cell in ONE run (the cell-sharding invariant)
+        heads = cell[np.concatenate(([0], np.flatnonzero(cell[1:] != cell[:-1]) + 1))]
+        if np.bincount(heads).max() > 1:
+            raise ValueError("gene rows of a record set need cell-sorted records (a cell barcode forms two runs)")
+    mito, multi = cols.gene_flags(mitochondrial_gene_ids)
+    dims = _dims(cols)
+    with DeviceGroup(devices) as g:
+        bounds = D.shard_bounds(cell, g.size)
+        g.comms()
+
+        def rank_rows(r):
+            lo, hi = bounds[r]
+            eng = g.engines[r]
+            dev_cols = E.to_device(_shard_arrays(cols.arrays, lo, hi), eng.device)
+            gm = torch.from_numpy(mito).to(eng.device)
+            gx = torch.from_numpy(multi).to(eng.device)
+            if hi == lo:
+                part = torch.zeros((max(1, dims.n_gene_ids), N.SCT_NP), dtype=torch.int64, device=eng.device)
+                ci = np.zeros((0, N.SCT_NI), np.int64)
+                cf = np.zeros((0, N.SCT_NF), np.float64)
+            elif float_mode == "exact":  # one pass: cell rows and gene partials share the cell-view work
+                ci, cf, part = eng.cell_and_gene(dev_cols, dims, gm)
+                ci, cf = ci.cpu().numpy(), cf.cpu().numpy()
+            else:  # Welford cell rows (record order), exact-sum gene partials
+                ci, cf = eng.compute(dev_cols, "cell", dims, gm, gx, float_mode=float_mode)
+                ci, cf = ci.cpu().numpy(), cf.cpu().numpy()
+                part = eng.gene_partials(dev_cols, dims)
+            if ci.shape[0]:
+                ci[:, N.I_ENTITY] += lo
+            g.allreduce_partials(r, part)  # RCCL over xGMI: every rank now holds the sums
+            gene = None
+            if r == 0:
+                gi, gf = eng.finalize_partials(part)
+                gene = (gi.cpu().numpy(), gf.cpu().numpy())
+            return ci, cf, gene
+
+        parts = g.run(rank_rows)
+    cell = (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
+    return cell, parts[0][2]

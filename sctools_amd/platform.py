@@ -11,7 +11,12 @@ codes as the reference's ``GenericPlatform`` metric commands
   CreateCountMatrix -b BAM -o PREFIX -a GTF [-c TAG -m TAG -g TAG -n]   (platform.py:384-470)
   MergeCountMatrices -i PREFIX... -o STEM                              (platform.py:475-516)
 
-New flags are optional only: ``--float-mode {welford,exact}`` and ``--device``.
+New flags are optional only: ``--float-mode {welford,exact}``, ``--device``, ``--devices N``
+(spread the entity runs over GPUs 0..N-1, one host thread each; same output) and, on
+CalculateCellMetrics, ``--gene-output-filestem STEM`` (also write the gene rows of the same
+cell-sorted file, as TagSortBam by gene + CalculateGeneMetrics would give them; with
+``--devices N`` the per-device gene partials are summed by an RCCL all-reduce -- the
+SplitBam / MergeGeneMetrics workflow in one command).
 Run as ``python -m sctools_amd <Command> [args]``.
 """
 
@@ -25,6 +30,8 @@ def _engine_args(parser):
     parser.add_argument("--float-mode", default="welford", choices=["welford", "exact"],
                         help="welford: bit-identical to sctools (default); exact: order-free exact sums")
     parser.add_argument("--device", default=None, help="torch device (default: current GPU)")
+    parser.add_argument("--devices", type=int, default=None,
+                        help="spread the work over GPUs 0..N-1 (one host thread each); output unchanged")
 
 
 class GenericPlatform:
@@ -36,7 +43,8 @@ class GenericPlatform:
         _engine_args(parser)
         args = parser.parse_args(args) if args is not None else parser.parse_args()
         g = metrics.gatherer.GatherGeneMetrics(args.input_bam, args.output_filestem,
-                                               float_mode=args.float_mode, device=args.device)
+                                               float_mode=args.float_mode, device=args.device,
+                                               devices=args.devices)
         g.extract_metrics()
         return 0
 
@@ -47,13 +55,22 @@ class GenericPlatform:
         parser.add_argument("-o", "--output-filestem", required=True, help="Output file stem.")
         parser.add_argument("-a", "--gtf-annotation-file", required=False, default=None,
                             help="gtf annotation file that bam_file was aligned against")
+        parser.add_argument("--gene-output-filestem", default=None,
+                            help="also write the gene metrics of this cell-sorted file (grouped by gene, "
+                                 "exact-sum floats) from the same pass")
         _engine_args(parser)
         args = parser.parse_args(args) if args is not None else parser.parse_args()
         mito: Set[str] = set()
         if args.gtf_annotation_file:
             mito = gtf.get_mitochondrial_gene_names(args.gtf_annotation_file)
-        g = metrics.gatherer.GatherCellMetrics(args.input_bam, args.output_filestem, mito,
-                                               float_mode=args.float_mode, device=args.device)
+        if args.gene_output_filestem:
+            g = metrics.gatherer.GatherCellAndGeneMetrics(args.input_bam, args.output_filestem,
+                                                          args.gene_output_filestem, mito,
+                                                          float_mode=args.float_mode, devices=args.devices or 1)
+        else:
+            g = metrics.gatherer.GatherCellMetrics(args.input_bam, args.output_filestem, mito,
+                                                   float_mode=args.float_mode, device=args.device,
+                                                   devices=args.devices)
         g.extract_metrics()
         return 0
 

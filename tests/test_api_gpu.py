@@ -108,3 +108,87 @@ def test_aggregator_protocol(kind):
             assert str(v) == row[col], (name, col)
         checked += 1
     assert checked >= 4
+
+
+@pytest.mark.parametrize("bam", H.BAMS)
+@pytest.mark.parametrize("kind", ["cell", "gene"])
+def test_gatherers_multi_device_path_matches_reference(tmp_path, bam, kind):
+    """devices=N (every visible GPU; N=1 on a one-GPU box): the sharded, threaded path gives the
+    reference's CSV byte for byte."""
+    import torch
+
+    from sctools_amd.metrics import GatherCellMetrics, GatherGeneMetrics
+
+    cls = GatherCellMetrics if kind == "cell" else GatherGeneMetrics
+    stem = str(tmp_path / "out")
+    cls(os.path.join(BAM_DIR, bam + ".bam"), stem, compress=False,
+        devices=torch.cuda.device_count()).extract_metrics()
+    assert _read(stem + ".csv") == H.golden_text(bam, kind)
+
+
+def test_cli_devices_flag(tmp_path):
+    from sctools_amd.platform import GenericPlatform
+
+    stem = str(tmp_path / "c")
+    assert GenericPlatform.calculate_cell_metrics(
+        ["-i", os.path.join(BAM_DIR, "small-cell-sorted.bam"), "-o", stem, "--devices", "1"]) == 0
+    assert _read(stem + ".csv.gz") == H.golden_text("small-cell-sorted", "cell")
+    stem = str(tmp_path / "g")
+    assert GenericPlatform.calculate_gene_metrics(
+        ["-i", os.path.join(BAM_DIR, "small-gene-sorted.bam"), "-o", stem, "--devices", "1"]) == 0
+    assert _read(stem + ".csv.gz") == H.golden_text("small-gene-sorted", "gene")
+
+
+@pytest.mark.parametrize("float_mode", ["welford", "exact"])
+def test_cell_and_gene_rows_from_one_cell_sorted_pass(tmp_path, float_mode):
+    """CalculateCellMetrics --gene-output-filestem on the reference's cell-sorted fixture: the cell
+    CSV is the reference's (byte for byte in Welford mode); the gene CSV is what the reference
+    writes for the SAME reads sorted by gene (small-gene-sorted.bam): integers and row order
+    exact, floats within 1e-9 (exact sums vs the reference's Welford in its file order).  The
+    gene partials pass through sct_allreduce_gene_partials (RCCL) even on one device."""
+    from sctools_amd.platform import GenericPlatform
+
+    cstem, gstem = str(tmp_path / "c"), str(tmp_path / "g")
+    assert GenericPlatform.calculate_cell_metrics(
+        ["-i", os.path.join(BAM_DIR, "cell-gene-umi-queryname-sorted.bam"), "-o", cstem,
+         "--gene-output-filestem", gstem, "--float-mode", float_mode, "--devices", "1"]) == 0
+    cell_want = H.golden_text("cell-gene-umi-queryname-sorted", "cell")
+    if float_mode == "welford":
+        assert _read(cstem + ".csv.gz") == cell_want
+    else:
+        H.assert_csv_close(_read(cstem + ".csv.gz"), cell_want, rel=1e-9)
+    H.assert_csv_close(_read(gstem + ".csv.gz"), H.golden_text("small-gene-sorted", "gene"), rel=1e-9)
+
+
+def test_cell_and_gene_rows_need_cell_sorted_input(tmp_path):
+    from sctools_amd.metrics import GatherCellAndGeneMetrics
+
+    with pytest.raises(ValueError, match="cell-sorted"):
+        GatherCellAndGeneMetrics(os.path.join(BAM_DIR, "unsorted.bam"), str(tmp_path / "c"),
+                                 str(tmp_path / "g")).extract_metrics()
+
+
+def test_allreduce_c_abi_with_own_communicator():
+    """The torch-free route: sct_comm_unique_id + sct_comm_init_rank + sct_allreduce_gene_partials
+    on a one-rank communicator leaves the partials unchanged (the sum over one rank)."""
+    import ctypes
+
+    import torch
+
+    from sctools_amd import _native as N
+
+    lib = N.load()
+    uid = (ctypes.c_uint8 * 128)()
+    N.check(lib.sct_comm_unique_id(uid, 128))
+    comm = ctypes.c_void_p()
+    N.check(lib.sct_comm_init_rank(ctypes.byref(comm), 1, uid, 128, 0, 0))
+    try:
+        part = torch.randint(-2**40, 2**40, (777, N.SCT_NP), dtype=torch.int64, device="cuda:0")
+        want = part.clone()
+        s = ctypes.c_void_p(torch.cuda.current_stream(part.device).cuda_stream)
+        N.check(lib.sct_allreduce_gene_partials(ctypes.c_void_p(part.data_ptr()), 777, comm, s))
+        torch.cuda.synchronize()
+        assert torch.equal(part, want)
+        assert lib.sct_allreduce_gene_partials(None, 5, comm, s) == -1
+    finally:
+        N.check(lib.sct_comm_destroy(comm))
