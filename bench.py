@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--records", type=int, default=100_000_000, help="records per rank")
     ap.add_argument("--cells", type=int, default=10_000, help="cells per rank")
     ap.add_argument("--genes", type=int, default=30_000)
+    ap.add_argument("--umi-bits", type=int, default=20,
+                    help="UMI ids in [0, 2^bits): 20 = 10-bp 10x v2 UMIs (default), 24 = 12-bp 10x v3")
     ap.add_argument("--float-mode", default="exact", choices=["exact", "welford"])
     ap.add_argument("--cpu-sample-s", type=float, default=15.0, help="target seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -85,6 +87,10 @@ def parse():
                     help="2: cell-sorted records (default); 4: the 1B-read atlas per GPU of 8 -- 125M records, 62.5k "
                          "cells with lognormal(0, 2) reads; 5: globally shuffled records, 30%% NH>1, 40%% duplicates, "
                          "sorted by cell on the GPU inside every step (SURVEY.md 8(d) configs 4, 5)")
+    ap.add_argument("--sort-order", default="cell_umi_gene", choices=["cell_umi_gene", "cell"],
+                    help="config 5: the order sorted inside every step -- (CB, UB, GE) then query name, as "
+                         "bam.sort_by_tags_and_queryname (bam.py:698-709) / TagSortBam define it (default), "
+                         "or CB only (all the cell and grouped gene metrics need)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"),
                     help="rocprofv3 --pmc per-kernel HBM bytes (tools/pmc_passes.sh) for roofline.traffic")
     return ap.parse_args()
@@ -116,15 +122,19 @@ def main():
     if args.config == 4:
         args.records, args.cells = 125_000_000, 62_500
     cfg = synth.SynthConfig(n_reads=args.records, n_cells=args.cells, n_genes=args.genes,
-                            sigma=2.0 if args.config == 4 else 1.0, seed=args.seed + 1000 * rank)
-    if args.config == 5:
-        cfg.p_nh1, cfg.p_dup = 0.70, 0.40
+                            sigma=2.0 if args.config == 4 else 1.0, seed=args.seed + 1000 * rank,
+                            umi_bits=args.umi_bits)
+    if args.config == 5:  # 30 % NH > 1, 40 % duplicates, secondary alignments sharing a query name
+        cfg.p_nh1, cfg.p_dup, cfg.p_secondary = 0.70, 0.40, 0.10
     data = synth.generate(cfg, device=dev, chunk=16_000_000)
-    if args.config == 5:  # global permutation: the step must regroup records by cell itself
+    qname, n_qnames = None, 0
+    if args.config == 5:  # global permutation: the step must regroup records itself
         g = torch.Generator(device=dev)
         g.manual_seed(args.seed + 1 + 1000 * rank)
         perm = torch.randperm(args.records, generator=g, device=dev)
         data.cols = {c: t[perm].contiguous() for c, t in data.cols.items()}
+        qname, n_qnames = data.extra["qname"][perm].contiguous(), data.extra["n_qnames"]
+        data.extra["qname"] = qname
         del perm
     torch.cuda.synchronize()
     if rank == 0:
@@ -132,8 +142,14 @@ def main():
     dims = E.Dims(data.n_cell_ids, data.n_gene_ids, data.n_umi_ids)
     mito = torch.from_numpy(data.gene_is_mito).to(dev)
     multi = torch.from_numpy(data.gene_is_multi).to(dev)
+    def regroup(cols):
+        """config 5: TagSortBam's order on the GPU (the step's first stage)."""
+        if args.sort_order == "cell":
+            return eng.tag_sort(cols, dims, "cell")
+        return eng.tag_sort(cols, dims, "cell_umi_gene", qname, n_qnames)
+
     if args.config == 5:
-        n_ent = eng.count_entities(eng.tag_sort(data.cols, dims, "cell"), "cell", dims)
+        n_ent = eng.count_entities(regroup(data.cols), "cell", dims)
     else:
         n_ent = eng.count_entities(data.cols, "cell", dims)
     partials = torch.empty((data.n_gene_ids, 64), dtype=torch.int64, device=dev)
@@ -145,7 +161,7 @@ def main():
     copy_stream = torch.cuda.Stream(device=dev)
 
     def step():
-        cols = eng.tag_sort(data.cols, dims, "cell") if args.config == 5 else data.cols
+        cols = regroup(data.cols) if args.config == 5 else data.cols
         if args.float_mode == "exact":
             # one pass: cell rows + grouped gene partials share the cell-view sort
             ci, cf, _ = eng.cell_and_gene(cols, dims, mito, n_entities=n_ent, partials=partials)
@@ -193,7 +209,7 @@ def main():
     eng.profile_only("")
     prof = eng.profile_read()
     elapsed = t1 - t0
-    side = side_measurements(eng, data, dims, mito, multi, args, dev) if rank == 0 else {}
+    side = side_measurements(eng, data, dims, mito, multi, args, regroup) if rank == 0 else {}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -254,13 +270,15 @@ def main():
             "config": {
                 "workload": ({2: "config2: %d cell-sorted records/rank",
                               4: "config4: %d cell-sorted records/rank, lognormal(0, 2) reads per cell",
-                              5: "config5: %d globally shuffled records/rank (30%% NH>1, 40%% dup), GPU sort by cell"}
+                              5: "config5: %d globally shuffled records/rank (30%% NH>1, 40%% dup, secondary alignments), "
+                                 "GPU sort by " + ("(CB, UB, GE, query name)" if args.sort_order != "cell" else "CB")}
                              [args.config]) % args.records + ", %d cells/rank, %d genes; cell metrics + grouped gene metrics%s"
                             % (args.cells, args.genes, " + RCCL all-reduce" if world > 1 else ""),
                 "records_per_rank": args.records,
                 "cells_per_rank": args.cells,
                 "genes": args.genes,
                 "float_mode": args.float_mode,
+                "umi_bits": args.umi_bits,
                 "parallelism": "cell-sharded x%d" % world,
             },
             "roofline": roofline,
@@ -278,7 +296,7 @@ def main():
         dist.destroy_process_group()
 
 
-def side_measurements(eng, data, dims, mito, multi, args, dev):
+def side_measurements(eng, data, dims, mito, multi, args, regroup):
     """Costs kept OUT of `value`, reported beside it:
     * the H2D copy of the 32-B SoA columns from pinned host memory (the bench generates its
       shard in HBM; a caller handing over host buffers pays this once per shard);
@@ -305,7 +323,7 @@ def side_measurements(eng, data, dims, mito, multi, args, dev):
     del dst, pinned
     out["h2d"] = {"ms": h2d_s * 1e3, "bytes": nbytes, "GB_per_s": nbytes / h2d_s / 1e9,
                   "note": "pinned host -> HBM copy of the SoA columns; excluded from value"}
-    cols = data.cols if args.config != 5 else eng.tag_sort(data.cols, dims, "cell")
+    cols = data.cols if args.config != 5 else regroup(data.cols)
     eng.count_entities(cols, "cell", dims)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -353,6 +371,7 @@ def cpu_baseline(data, args):
             h = {c: t[:n].cpu().numpy() for c, t in cols.items()}
             for c in ("gq_sum", "gq_len", "gq_gt30"):
                 h[c] = h[c].view(np.uint16)
+            h["_qname"] = data.extra["qname"][:n].cpu().numpy()
             return n, h
         # cut at a cell boundary so every cell in the sample is complete
         c_last = int(cell[n - 1].item())
@@ -365,9 +384,12 @@ def cpu_baseline(data, args):
 
     def run(h):
         t0 = time.perf_counter()
-        if args.config == 5:  # regroup by cell first, as the GPU step does (numpy stable sort)
-            order = np.argsort(h["cell"], kind="stable")
-            h = {c: a[order] for c, a in h.items()}
+        if args.config == 5:  # the GPU step's sort first: numpy's stable lexsort, as sorted() orders
+            if args.sort_order == "cell":
+                order = np.argsort(h["cell"], kind="stable")
+            else:
+                order = np.lexsort((h["_qname"], h["gene"], h["umi"], h["cell"]))
+            h = {c: a[order] for c, a in h.items() if c != "_qname"}
         O.run(h, "cell", data.gene_is_mito, data.n_gene_ids, threads=threads)
         O.run(h, "gene_grouped", data.gene_is_mito, data.n_gene_ids, threads=threads)
         return time.perf_counter() - t0
@@ -384,8 +406,9 @@ def cpu_baseline(data, args):
         "kind": "port",
         "sample": ("first %d records (%d whole cells) of rank 0's shard: oracle cell metrics + grouped gene "
                    "metrics, %.1fs" % (n1, int(h1["cell"][-1]) + 1, t1)) if args.config != 5 else
-                  ("first %d records of rank 0's shuffled shard: numpy stable sort by cell + oracle cell metrics + "
-                   "grouped gene metrics, %.1fs" % (n1, t1)),
+                  ("first %d records of rank 0's shuffled shard: numpy stable %s + oracle cell metrics + "
+                   "grouped gene metrics, %.1fs" % (n1, "sort by cell" if args.sort_order == "cell" else
+                                                    "lexsort by (CB, UB, GE, query name)", t1)),
     }
 
 

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "../../include/sct_bam.h"
+#include "bgzf.h"
 
 namespace {
 
@@ -63,17 +64,6 @@ enum : uint8_t {
   B_PERFECT_CB = 1u << 7,
 };
 enum : uint8_t { XF_ABSENT = 0, XF_CODING, XF_INTRONIC, XF_UTR, XF_INTERGENIC, XF_OTHER };
-
-inline uint16_t rd16(const uint8_t* p) {
-  uint16_t v;
-  memcpy(&v, p, 2);
-  return v;
-}
-inline uint32_t rd32(const uint8_t* p) {
-  uint32_t v;
-  memcpy(&v, p, 4);
-  return v;
-}
 
 // ---------------- string interning ----------------
 inline uint64_t hash_bytes(const char* p, size_t n) {
@@ -145,48 +135,6 @@ class Interner {
   Stripe stripes_[kStripes];
   std::atomic<int32_t> next_;
 };
-
-// ---------------- BGZF ----------------
-struct Block {
-  uint64_t off;
-  uint32_t csize, isize;
-};
-
-int scan_blocks(const uint8_t* f, uint64_t size, std::vector<Block>& blocks) {
-  uint64_t off = 0;
-  while (off < size) {
-    if (size - off < 18 || f[off] != 31 || f[off + 1] != 139 || f[off + 2] != 8 || !(f[off + 3] & 4))
-      return fail(SCT_BAM_EFORMAT, "not a BGZF block at byte %llu", (unsigned long long)off);
-    const uint16_t xlen = rd16(f + off + 10);
-    uint64_t p = off + 12, end = off + 12 + xlen;
-    int64_t bsize = -1;
-    while (p + 4 <= end) {
-      const uint16_t slen = rd16(f + p + 2);
-      if (f[p] == 66 && f[p + 1] == 67 && slen == 2) bsize = rd16(f + p + 4);
-      p += 4 + slen;
-    }
-    if (bsize < 0 || off + (uint64_t)bsize + 1 > size)
-      return fail(SCT_BAM_EFORMAT, "bad BGZF block size at byte %llu", (unsigned long long)off);
-    const uint32_t csize = (uint32_t)bsize + 1;
-    const uint32_t isize = rd32(f + off + csize - 4);
-    blocks.push_back(Block{off, csize, isize});
-    off += csize;
-  }
-  return SCT_BAM_OK;
-}
-
-bool inflate_block(const uint8_t* f, const Block& b, uint8_t* out, z_stream& z) {
-  const uint16_t xlen = rd16(f + b.off + 10);
-  const uint64_t data = b.off + 12 + xlen;
-  const uint32_t clen = b.csize - 12 - xlen - 8;
-  if (inflateReset(&z) != Z_OK) return false;
-  z.next_in = const_cast<Bytef*>(f + data);
-  z.avail_in = clen;
-  z.next_out = out;
-  z.avail_out = b.isize;
-  const int rc = inflate(&z, Z_FINISH);
-  return rc == Z_STREAM_END && z.avail_out == 0;
-}
 
 // ---------------- records ----------------
 struct Columns {

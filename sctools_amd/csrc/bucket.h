@@ -26,10 +26,11 @@
 // group's ">= 2 records" event.
 //
 // Records travel as a 16-byte payload (two u64 words, SoA) so no pass gathers by index:
-//   w0 = key' << 24 | ref (17 bits) << 7 | strand << 6 | mapped << 5 | k1 is mitochondrial << 4
+//   w0 = key' << 17 | ref (14 bits) << 3 | strand << 2 | mapped << 1 | k1 is mitochondrial
 //   w1 = record index << 32 | pos (uint32)
 // key' = [k1' | k2 | hash] with k1' = k1 * odd mod 2^k1 (Bits::scramble), so heavy genes with
-// neighbouring ids do not pile into one top digit.  KB = k1 + k2 + h <= 40.
+// neighbouring ids do not pile into one top digit.  KB = k1 + k2 + h <= 47 (so a 10x-v3 shard,
+// 2^24 UMIs and ~2^17 gene ids, stays on this path); a mapped ref id must be < 2^14.
 #pragma once
 #include <type_traits>
 
@@ -44,11 +45,12 @@ constexpr int kBCap = kWin - 1;             // records of a terminal bucket
 constexpr int kTileCap = kWin + kBCap - 1;  // records per tile at most (2046)
 constexpr int kChunk = 2048;                // records per partition work item (LDS-staged)
 constexpr int kChunkItems = kChunk / kBlock;
-constexpr int kMaxKeyBits = 40;             // KB <= 40: key' sits in w0 bits [63:24]
-constexpr int kKeyShift = 24;
-constexpr int kRefBits = 17;                // mapped reference ids must be < 2^17
-constexpr uint64_t kW0Mapped = 1ull << 5;
-constexpr uint64_t kW0Mito = 1ull << 4;
+constexpr int kMaxKeyBits = 47;             // KB <= 47: key' sits in w0 bits [63:17]
+constexpr int kKeyShift = 17;
+constexpr int kRefBits = 14;                // mapped reference ids must be < 2^14
+constexpr int kFragBits = kRefBits + 1;     // (ref, strand) of a payload
+constexpr uint64_t kW0Mapped = 1ull << 1;
+constexpr uint64_t kW0Mito = 1ull << 0;
 constexpr int kHBlock = 512;                // tile block: two window positions per thread
 constexpr int kHWaves = kHBlock / kWave;
 constexpr int kHTBits = 11;
@@ -67,6 +69,8 @@ static_assert(kBigCap < kBigSlots && kBigSlots <= 4096, "big-bucket keys fit its
 static_assert(kWin == 2 * kHBlock && (1 << kWinBits) == kWin, "window layout");
 static_assert(kBCap < (1 << 11), "count field");
 static_assert(kHTSlots <= 4096, "molecule slots are 12 bits in the fragment key");
+static_assert(12 + kFragBits + 32 + 2 <= 64, "fragment key: molecule slot, (ref, strand), pos, 2 state bits");
+static_assert(kWinBits + kMaxKeyBits + 2 <= 64, "molecule key: window offset, key bits, 2 state bits");
 
 // terminal bucket descriptor, stored (u16) at the bucket's first record position
 enum : uint16_t {
@@ -90,11 +94,13 @@ struct BucketCtl {  // device counters of one level (n_giant, n_big accumulate o
 };
 
 __device__ __forceinline__ uint64_t payload_w0(uint64_t key, int32_t ref, bool reverse, bool mapped, bool mito) {
-  return (key << kKeyShift) | ((uint64_t)((uint32_t)ref & ((1u << kRefBits) - 1)) << 7) |
-         ((uint64_t)(reverse ? 1 : 0) << 6) | (mapped ? kW0Mapped : 0ull) | (mito ? kW0Mito : 0ull);
+  return (key << kKeyShift) | ((uint64_t)((uint32_t)ref & ((1u << kRefBits) - 1)) << 3) |
+         ((uint64_t)(reverse ? 1 : 0) << 2) | (mapped ? kW0Mapped : 0ull) | (mito ? kW0Mito : 0ull);
 }
-// fragment identity (ref, strand) of a payload: 18 bits
-__device__ __forceinline__ uint32_t payload_frag(uint64_t w0) { return (uint32_t)(w0 >> 6) & 0x3FFFFu; }
+// fragment identity (ref, strand) of a payload: kFragBits bits
+__device__ __forceinline__ uint32_t payload_frag(uint64_t w0) {
+  return (uint32_t)(w0 >> 2) & ((1u << kFragBits) - 1);
+}
 
 __device__ __forceinline__ void push_segment(const Seg& sg, Seg* __restrict__ seg, Work* __restrict__ work,
                                              BucketCtl* ctl) {
@@ -459,7 +465,7 @@ __global__ void __launch_bounds__(kHBlock) k_hash_tile(const uint16_t* __restric
     // events: that group's inserter and first finder are among the molecule's first two records.
     if (em != 0) ht_insert<K1E>(s_k1, (K1E)((((uint64_t)bs << b.k1) | (key >> sh_k1)) << 2), ek);
     if (x0 & kW0Mapped) {
-      const uint64_t fk = ((((uint64_t)ms << 18) | payload_frag(x0)) << 32) | (uint32_t)x1;
+      const uint64_t fk = ((((uint64_t)ms << kFragBits) | payload_frag(x0)) << 32) | (uint32_t)x1;
       ht_insert<unsigned long long>(s_frg, fk << 2, ef);
     }
     // split groups: only the first piece counts the head, and it also carries the multi event
@@ -532,7 +538,7 @@ __global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict_
     const uint32_t ms = ht_insert<unsigned long long>(s_mol, (key >> sh_mol) << 2, em, tb);
     if (em != 0) ht_insert<K1E>(s_k1, (K1E)((key >> sh_k1) << 2), ek, tb);  // as in k_hash_tile
     if (x0 & kW0Mapped) {
-      const uint64_t fk = ((((uint64_t)ms << 18) | payload_frag(x0)) << 32) | (uint32_t)x1;
+      const uint64_t fk = ((((uint64_t)ms << kFragBits) | payload_frag(x0)) << 32) | (uint32_t)x1;
       ht_insert<unsigned long long>(s_frg, fk << 2, ef, tb);
     }
     const bool k1_head = ek == 1 && !(bd & BD_K1_NOHEAD);

@@ -45,7 +45,7 @@ namespace {
 struct Layout {
   size_t tile_cnt, scalars, scan_sums, keys_a, keys_b, vals_a, vals_b, counts, offsets, ent_start, partials;
   size_t gcounts, gcursor, gwork, dflags, gpay, seen, zero_mito;
-  size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, bigs, total;
+  size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, bigs, wctl, worder, total;
   int64_t num_tiles, num_chunks, max_ent, max_gene_work, max_seg, max_work;
   int n_buckets;
   bool gene;
@@ -100,6 +100,9 @@ Layout layout_for(const sct_plan_t* plan) {
   L.seg_cur = take(sizeof(uint32_t) * kRadix * (size_t)L.max_seg);
   L.giants = take(sizeof(Seg) * (size_t)L.max_seg);
   L.bigs = take(sizeof(Seg) * (size_t)L.max_seg);
+  const bool welford = plan->float_mode == SCT_FLOAT_WELFORD;
+  L.wctl = take(welford ? sizeof(WelfordCtl) : 0);
+  L.worder = take(welford ? sizeof(uint32_t) * (size_t)L.max_ent : 0);
   L.total = off;
   return L;
 }
@@ -425,13 +428,27 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   if (out_i) {
     LAUNCH("finalize", k_finalize, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, (const int64_t*)partials,
            n_ent, cell ? SCT_MODE_CELL : SCT_MODE_GENE, exact ? 1 : 0, (const int64_t*)ent_start, out_i, out_f);
-    if (!exact) {
+    if (!exact) {  // sequential Welford: big entities one wave each (largest first), small ones a lane each
+      const dim3 egrid((unsigned)cdiv(n_ent, kBlock));
+      if (n >= kWfWave) {
+        WelfordCtl* wc = at<WelfordCtl>(ws, L.wctl);
+        uint32_t* worder = at<uint32_t>(ws, L.worder);
+        HIPCHK(hipMemsetAsync(wc, 0, sizeof(WelfordCtl), s));
+        LAUNCH("welford_bins", k_welford_bins, egrid, dim3(kBlock), s, (const int64_t*)ent_start, n_ent, n, wc);
+        LAUNCH("welford_order", k_welford_order, egrid, dim3(kBlock), s, (const int64_t*)ent_start, n_ent, n, wc,
+               worder);
+        if (cell) {
+          LAUNCH("welford_wave", k_welford_wave<true>, dim3(kWfBlocks), dim3(kBlock), s, rc2,
+                 (const int64_t*)ent_start, n_ent, n, (const uint32_t*)worder, wc, out_f);
+        } else {
+          LAUNCH("welford_wave", k_welford_wave<false>, dim3(kWfBlocks), dim3(kBlock), s, rc2,
+                 (const int64_t*)ent_start, n_ent, n, (const uint32_t*)worder, wc, out_f);
+        }
+      }
       if (cell) {
-        LAUNCH("welford", k_welford<true>, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, rc2,
-               (const int64_t*)ent_start, n_ent, n, out_f);
+        LAUNCH("welford", k_welford<true>, egrid, dim3(kBlock), s, rc2, (const int64_t*)ent_start, n_ent, n, out_f);
       } else {
-        LAUNCH("welford", k_welford<false>, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, rc2,
-               (const int64_t*)ent_start, n_ent, n, out_f);
+        LAUNCH("welford", k_welford<false>, egrid, dim3(kBlock), s, rc2, (const int64_t*)ent_start, n_ent, n, out_f);
       }
     }
   }

@@ -63,6 +63,7 @@ class SynthConfig:
     p_bad_ub: float = 0.002
     p_none_cell_reads: float = 0.0  # fraction of reads emitted as a leading CB=None run
     p_secondary: float = 0.0  # records that are a secondary alignment of the previous read (config 5)
+    umi_bits: int = 20  # UMI ids uniform in [0, 2^umi_bits): 20 = 10-bp 10x v2 UMIs, 24 = 12-bp 10x v3
     keep_qualities: bool = False  # keep per-base aligned qualities (fixtures only)
 
 
@@ -198,7 +199,7 @@ def generate(cfg: SynthConfig, device="cpu", chunk: int = 8_000_000) -> SynthDat
     gsel = torch.rand(n_mol, generator=gen, device=dev, dtype=torch.float64)
     mol_gene = torch.where(gsel < cfg.p_none_gene, torch.zeros_like(grank),
                            torch.where(gsel < cfg.p_none_gene + cfg.p_multi_gene, mr2i[grank], r2i[grank]))
-    mol_umi = torch.randint(0, 1 << 20, (n_mol,), generator=gen, device=dev, dtype=torch.int64)
+    mol_umi = torch.randint(0, 1 << cfg.umi_bits, (n_mol,), generator=gen, device=dev, dtype=torch.int64)
     mol_ref = torch.randint(0, 25, (n_mol,), generator=gen, device=dev, dtype=torch.int64)
     mol_anchor = torch.randint(0, 1 << 27, (n_mol,), generator=gen, device=dev, dtype=torch.int64)
 
@@ -300,7 +301,7 @@ def generate(cfg: SynthConfig, device="cpu", chunk: int = 8_000_000) -> SynthDat
         cols=cols,
         n_cell_ids=cfg.n_cells + (1 if has_none else 0),
         n_gene_ids=len(names),
-        n_umi_ids=1 << 20,
+        n_umi_ids=1 << cfg.umi_bits,
         gene_names=names,
         gene_is_mito=gene_is_mito,
         gene_is_multi=gene_is_multi,

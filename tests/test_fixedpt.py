@@ -107,3 +107,13 @@ def test_division_free_quotient_is_exact():
     tot, bad = (int(v) for v in out.stdout.split())
     assert tot == 65535 * 65536
     assert bad == 0 and out.returncode == 0
+
+
+def test_welford_chain_division_is_ieee(tmp_path):
+    """k_welford_wave divides by the record count as RN(q0 + r y) (finalize.h); it must be the
+    IEEE quotient for every delta / k the chain can meet (checked on 20M random cases here)."""
+    exe = str(tmp_path / "welfdiv")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", exe, os.path.join(HERE, "native", "welfdiv.c"), "-lm"],
+                   check=True)
+    out = subprocess.run([exe, "20000000", "7"], check=True, capture_output=True, text=True).stdout
+    assert out.strip().splitlines()[-1] == "0", out

@@ -51,7 +51,7 @@ def colliding_pos(ref, pos, hbits, start=5000):
 
 def craft(n_gene_ids, n_umi_ids, seed):
     rng = np.random.default_rng(seed)
-    hbits = min(8, 40 - bitlen(n_gene_ids) - bitlen(n_umi_ids))
+    hbits = min(8, 47 - bitlen(n_gene_ids) - bitlen(n_umi_ids))  # bucket.h kMaxKeyBits
     rows = []  # (cell, gene, umi, ref, pos, unmapped)
 
     def add(cell, gene, umi, ref, pos, unmapped=False, k=1):
@@ -156,7 +156,8 @@ def run_all(eng, arrays, mito, n_cells, n_gene_ids, n_umi_ids):
     return out
 
 
-@pytest.mark.parametrize("n_gene_ids,n_umi_ids,seed", [(50, 100, 1), (30_000, 1 << 20, 2)])
+@pytest.mark.parametrize("n_gene_ids,n_umi_ids,seed", [(50, 100, 1), (30_000, 1 << 20, 2),
+                                                       (120_000, 1 << 24, 5)])  # 10x v3: 12-bp UMIs
 def test_bucket_edge_cases_match_oracle(eng, n_gene_ids, n_umi_ids, seed):
     arrays, mito, n_cells = craft(n_gene_ids, n_umi_ids, seed)
     got = run_all(eng, arrays, mito, n_cells, n_gene_ids, n_umi_ids)
@@ -226,3 +227,59 @@ def test_run_count_aligned_and_misaligned_columns(eng, n):
         cols["cell"] = buf[shift:shift + n]
         assert (cols["cell"].data_ptr() % 16 == 0) == (shift == 0)
         assert eng.count_entities(cols, "cell", dims) == want, shift
+
+
+def kernels_run(eng, fn):
+    eng.profile_only("")
+    eng.profile_enable(True)
+    try:
+        fn()
+        torch.cuda.synchronize()
+    finally:
+        eng.profile_enable(False)
+    return set(eng.profile_read())
+
+
+def test_10x_v3_shard_stays_on_the_bucket_path(eng):
+    """k1 + k2 = 17 + 24 bits (2^24 UMI ids, 120k gene ids) fits the 47-bit bucket key: no
+    device-wide LSD sort runs, and the rows match the oracle."""
+    from sctools_amd import engine as E
+    from sctools_amd import synth
+
+    d = synth.generate(synth.SynthConfig(n_reads=2_000_000, n_cells=300, n_genes=60_000, seed=12, umi_bits=24),
+                       device=eng.device)
+    assert d.n_umi_ids == 1 << 24 and d.n_gene_ids > 1 << 16
+    dims = E.Dims(d.n_cell_ids, d.n_gene_ids, d.n_umi_ids)
+    mito = torch.from_numpy(d.gene_is_mito).to(eng.device)
+    out = {}
+    ran = kernels_run(eng, lambda: out.update(zip(("ci", "cf", "p"), eng.cell_and_gene(d.cols, dims, mito))))
+    assert "hash_tile" in ran and not any(k.startswith("radix") for k in ran), ran
+    h = {c: t.cpu().numpy() for c, t in d.cols.items()}
+    for c in ("gq_sum", "gq_len", "gq_gt30"):
+        h[c] = h[c].view(np.uint16)
+    oi, of = O.run(h, "cell", d.gene_is_mito, d.n_gene_ids, threads=8)
+    compare(out["ci"].cpu().numpy(), out["cf"].cpu().numpy(), oi, of, exact=False)
+    gi, gf = eng.finalize_partials(out["p"])
+    oi, of = O.run(h, "gene_grouped", d.gene_is_mito, d.n_gene_ids, threads=8)
+    live = oi[:, 0] > 0
+    compare(gi.cpu().numpy()[live], gf.cpu().numpy()[live], oi[live], of[live], exact=False)
+
+
+def test_reference_ids_beyond_the_payload_fall_back_to_the_global_sort(eng):
+    """A mapped ref id >= 2^14 does not fit the bucket payload: the call reruns on the LSD-sort
+    path and the rows still match the oracle."""
+    from sctools_amd import engine as E
+
+    arrays, mito, n_cells = craft(300, 4096, 6)
+    arrays = {k: v.copy() for k, v in arrays.items()}
+    mapped = arrays["ref"] >= 0
+    arrays["ref"][mapped] += 20_000
+    dims = E.Dims(n_cells, 300, 4096)
+    cols = E.to_device(arrays, eng.device)
+    gm = torch.from_numpy(mito).to(eng.device)
+    out = {}
+    ran = kernels_run(eng, lambda: out.update(zip(("i", "f"), eng.compute(cols, "cell", dims, gm, gm,
+                                                                           float_mode="welford"))))
+    assert any(k.startswith("radix") for k in ran), ran
+    oi, of = O.run(arrays, "cell", mito, 300, threads=8)
+    compare(out["i"].cpu().numpy(), out["f"].cpu().numpy(), oi, of, exact=True)
