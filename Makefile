@@ -13,8 +13,8 @@ all: $(ENGINE) $(BAMDEC) $(CSVFMT) oracle/liboracle.so tests/native/libfxcheck.s
 $(ENGINE): $(SRC) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC) -L/opt/rocm/lib -lrccl
 
-$(BAMDEC): sctools_amd/csrc/bamdec.cpp include/sct_bam.h
-	g++ -O3 -std=c++17 -fopenmp -fPIC -shared -Wall -o $@ sctools_amd/csrc/bamdec.cpp -lz
+$(BAMDEC): sctools_amd/csrc/bamdec.cpp sctools_amd/csrc/bamsplit.cpp sctools_amd/csrc/bgzf.h include/sct_bam.h
+	g++ -O3 -std=c++17 -fopenmp -fPIC -shared -Wall -o $@ sctools_amd/csrc/bamdec.cpp sctools_amd/csrc/bamsplit.cpp -lz
 
 $(CSVFMT): sctools_amd/csrc/csvfmt.cpp include/sct_csv.h
 	g++ -O3 -std=c++17 -fopenmp -fPIC -shared -Wall -o $@ sctools_amd/csrc/csvfmt.cpp -lz

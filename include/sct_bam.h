@@ -30,6 +30,7 @@ extern "C" {
 #define SCT_BAM_ZERODIV -12     /* empty quality string (ZeroDivisionError)         */
 #define SCT_BAM_VALUEERROR -13  /* invalid clipping, or a record beyond the 32-byte columnar limits */
 #define SCT_BAM_EMPTY -14       /* no records (RuntimeError: StopIteration in iter_tag_groups) */
+#define SCT_BAM_MISSING_TAG -15 /* sct_bam_split: a record carries none of the tags (RuntimeError, bam.py:286-289) */
 
 #define SCT_BAM_CELL_METRICS 0 /* require CY (and CR where CB is present), as CellMetrics does   */
 #define SCT_BAM_GENE_METRICS 1 /* records of multi-gene GE values are not validated (gatherer.py:210-212) */
@@ -75,6 +76,21 @@ int sct_bam_dictionary(const sct_bam_t* b, int32_t which, int64_t* n, const char
                        const int64_t** offsets, int32_t* has_none);
 
 void sct_bam_close(sct_bam_t* b);
+
+/* SplitBam (bam.split, bam.py:361-488; platform.py:153-223): the records of the input BAMs
+ * into chunk files `<out_prefix>_<k>.bam`, k = 0 .. *n_out - 1, every barcode in exactly one
+ * chunk.  A record's barcode is the value of the first of the `n_tags` two-character tags in
+ * `tags` (priority order, e.g. "CBCR") it carries; records with none raise
+ * SCT_BAM_MISSING_TAG when raise_missing, else they are dropped.  Barcodes are ranked in
+ * string order and chunk k gets the barcodes of rank k (mod n_subfiles when there are more
+ * barcodes than chunks), so *n_out = min(#barcodes, n_subfiles).  Records keep their file
+ * order; several inputs (same reference list) are concatenated in input order.  Each chunk is
+ * a BGZF file: the first input's header, the records (deflate `level` 0-9, 6 as htslib's
+ * default), the EOF member.  n_threads <= 0: all cores.  On an error *bad_record (if set) is
+ * the offending record's index over all inputs. */
+int sct_bam_split(const char* const* in_paths, int32_t n_in, const char* out_prefix, const char* tags,
+                  int32_t n_tags, int32_t n_subfiles, int32_t raise_missing, int32_t level, int32_t n_threads,
+                  int32_t* n_out, int64_t* bad_record);
 
 #ifdef __cplusplus
 }

@@ -17,15 +17,26 @@ reference's ``MetricAggregator.parse_molecule`` depends on
 * ``get_tag``: ``KeyError`` for an absent tag.
 
 BGZF is a concatenation of gzip members, so it is inflated with ``zlib`` in
-streaming fashion.  A native multi-threaded decoder is the SURVEY §8(f) #1
-follow-up; this reader is what the fixtures and the drop-in API use today.
+streaming fashion.  It decodes SAM input and is the decoder the tests compare the
+native one against; BAM input of the metric path goes through the native
+multi-threaded decoder (``sctools_amd/csrc/bamdec.cpp``).
+
+``split`` is SplitBam (``bam.py:361-488``) on the native splitter
+(``sctools_amd/csrc/bamsplit.cpp``).
 """
 
+import math
+import os
 import struct
+import sys
+import warnings
 import zlib
-from typing import Dict, Iterator, List, Optional, Tuple
+from typing import Dict, Iterator, List, Optional, Set, Tuple
 
-__all__ = ["BamRecord", "open_alignments", "read_header"]
+from sctools_amd import consts
+
+__all__ = ["BamRecord", "open_alignments", "read_header", "split", "get_barcodes_from_bam",
+           "get_barcode_for_alignment"]
 
 _CIGAR_OPS = "MIDNSHP=X"
 _SEQ_NT16 = "=ACMGRSVTWYHKDBN"
@@ -327,3 +338,58 @@ def read_header(path: str) -> Tuple[str, List[Tuple[str, int]]]:
         return text, refs
     finally:
         stream.close()
+
+
+# ---------------- SplitBam (bam.py:236-488) ----------------
+def get_barcode_for_alignment(alignment, tags: List[str], raise_missing: bool):
+    """The value of the first of ``tags`` the alignment carries (bam.py:263-290)."""
+    barcode = None
+    for tag in tags:
+        if alignment.has_tag(tag):
+            barcode = alignment.get_tag(tag)
+            break
+    if raise_missing and barcode is None:
+        raise RuntimeError("Alignment encountered that is missing {} tag(s).".format(tags))
+    return barcode
+
+
+def get_barcodes_from_bam(in_bam: str, tags: List[str], raise_missing: bool) -> Set:
+    """Distinct barcodes of a BAM, None excluded (bam.py:236-260)."""
+    out = set()
+    for alignment in open_alignments(in_bam, "rb"):
+        b = get_barcode_for_alignment(alignment, tags, raise_missing)
+        if b is not None:
+            out.add(b)
+    return out
+
+
+def split(in_bams: List[str], out_prefix: str, tags: List[str], approx_mb_per_split: float = 1000,
+          raise_missing: bool = True, num_processes: Optional[int] = None) -> List[str]:
+    """SplitBam (bam.py:361-488): split ``in_bams`` by barcode into chunks of about
+    ``approx_mb_per_split`` MB, every barcode in exactly one chunk.
+
+    Same arguments, limits, errors and return value as the reference: ``ValueError`` for no
+    tags or too many chunks, ``RuntimeError`` for a record without any of ``tags`` when
+    ``raise_missing``, chunk paths ``realpath(f"{out_prefix}_{k}.bam")`` in chunk order.  The
+    work is one native call (sctools_amd/csrc/bamsplit.cpp) on ``num_processes`` threads.
+    Barcodes are assigned to chunks in string order (the reference uses Python set order, which
+    varies from run to run); records keep their file order; several inputs are concatenated.
+    """
+    from sctools_amd import bamnative
+
+    if len(tags) == 0:
+        raise ValueError("At least one tag must be passed")
+    if num_processes is None:
+        num_processes = os.cpu_count() or 1
+    bam_mb = sum(os.path.getsize(b) * 1e-6 for b in in_bams)
+    n_subfiles = int(math.ceil(bam_mb / approx_mb_per_split))
+    if n_subfiles > consts.MAX_BAM_SPLIT_SUBFILES_TO_WARN:
+        warnings.warn("Number of requested subfiles (%d) exceeds %d; this may cause OS errors by exceeding fid "
+                      "limits" % (n_subfiles, consts.MAX_BAM_SPLIT_SUBFILES_TO_WARN))
+    if n_subfiles > consts.MAX_BAM_SPLIT_SUBFILES_TO_RAISE:
+        raise ValueError("Number of requested subfiles (%d) exceeds %d; this will usually cause OS errors, think "
+                         "about increasing max_mb_per_split." % (n_subfiles, consts.MAX_BAM_SPLIT_SUBFILES_TO_RAISE))
+    sys.stderr.write("Splitting the bams by barcode\n")
+    n = bamnative.split(list(in_bams), out_prefix, list(tags), max(1, n_subfiles), raise_missing,
+                        threads=num_processes)
+    return [os.path.realpath("%s_%d.bam" % (out_prefix, k)) for k in range(n)]

@@ -19,11 +19,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libsct_bam.so")
 
 OK, EIO, EFORMAT = 0, -1, -2
-KEYERROR, TYPEERROR, ZERODIV, VALUEERROR, EMPTY = -10, -11, -12, -13, -14
+KEYERROR, TYPEERROR, ZERODIV, VALUEERROR, EMPTY, MISSING_TAG = -10, -11, -12, -13, -14, -15
 CELL_METRICS, GENE_METRICS, COUNT_MATRIX = 0, 1, 2
 _MODES = {"cell": CELL_METRICS, "gene": GENE_METRICS, "count": COUNT_MATRIX}
 EXPORTED = ("sct_bam_decode", "sct_bam_decode_tags", "sct_bam_last_error", "sct_bam_n", "sct_bam_column", "sct_bam_dictionary",
-            "sct_bam_close")
+            "sct_bam_close", "sct_bam_split")
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -53,6 +53,10 @@ def load() -> ctypes.CDLL:
                                      ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int32)]
     L.sct_bam_close.restype = None
     L.sct_bam_close.argtypes = [vp]
+    i32 = ctypes.c_int32
+    L.sct_bam_split.restype = ctypes.c_int
+    L.sct_bam_split.argtypes = [ctypes.POINTER(ctypes.c_char_p), i32, ctypes.c_char_p, ctypes.c_char_p, i32, i32, i32,
+                                i32, i32, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_int64)]
     _lib = L
     return L
 
@@ -62,7 +66,7 @@ def available() -> bool:
 
 
 _EXC = {KEYERROR: KeyError, TYPEERROR: TypeError, ZERODIV: ZeroDivisionError, VALUEERROR: ValueError,
-        EMPTY: RuntimeError, EFORMAT: ValueError, EIO: OSError}
+        EMPTY: RuntimeError, EFORMAT: ValueError, EIO: OSError, MISSING_TAG: RuntimeError}
 
 
 def decode(path: str, metric_mode: str = "cell", threads: int = 0, tags=("CB", "UB", "GE")):
@@ -107,3 +111,21 @@ def decode(path: str, metric_mode: str = "cell", threads: int = 0, tags=("CB", "
         return arrays, names
     finally:
         L.sct_bam_close(h)
+
+
+def split(in_paths, out_prefix: str, tags, n_subfiles: int, raise_missing: bool = True, level: int = 6,
+          threads: int = 0) -> int:
+    """sct_bam_split: chunk files ``<out_prefix>_<k>.bam``; returns the number written."""
+    L = load()
+    for t in tags:
+        if len(t) != 2:
+            raise ValueError("tags must be two-character BAM tag names: %r" % (tags,))
+    arr = (ctypes.c_char_p * len(in_paths))(*[os.fsencode(p) for p in in_paths])
+    n_out = ctypes.c_int32(0)
+    bad = ctypes.c_int64(-1)
+    rc = L.sct_bam_split(arr, len(in_paths), os.fsencode(out_prefix), "".join(tags).encode(), len(tags),
+                         int(n_subfiles), 1 if raise_missing else 0, int(level), int(threads), ctypes.byref(n_out),
+                         ctypes.byref(bad))
+    if rc != OK:
+        raise _EXC.get(rc, RuntimeError)(L.sct_bam_last_error().decode("utf-8", "replace"))
+    return int(n_out.value)

@@ -39,19 +39,6 @@
 
 namespace {
 
-thread_local std::string g_err;
-
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return code;
-}
-
 // bits / xf codes: sctools_amd/columnar.py, include/sctools_gpu.h
 enum : uint8_t {
   B_UNMAPPED = 1u << 0,
@@ -65,77 +52,6 @@ enum : uint8_t {
 };
 enum : uint8_t { XF_ABSENT = 0, XF_CODING, XF_INTRONIC, XF_UTR, XF_INTERGENIC, XF_OTHER };
 
-// ---------------- string interning ----------------
-inline uint64_t hash_bytes(const char* p, size_t n) {
-  uint64_t h = 1469598103934665603ull;  // FNV-1a, then a mix
-  for (size_t i = 0; i < n; i++) h = (h ^ (uint8_t)p[i]) * 1099511628211ull;
-  h ^= h >> 29;
-  h *= 0xBF58476D1CE4E5B9ull;
-  h ^= h >> 32;
-  return h;
-}
-
-class Interner {
- public:
-  static constexpr int kStripes = 256;
-  Interner() : next_(1) {}
-  // provisional id >= 1 of the string
-  int32_t intern(const char* p, size_t n) { return intern(p, n, hash_bytes(p, n)); }
-  int32_t intern(const char* p, size_t n, uint64_t h) {
-    Stripe& s = stripes_[h & (kStripes - 1)];
-    std::lock_guard<std::mutex> lk(s.m);
-    if (s.slots.empty()) s.slots.assign(64, Slot{0, 0, 0, 0});
-    size_t mask = s.slots.size() - 1;
-    size_t i = (h >> 8) & mask;
-    while (true) {
-      Slot& e = s.slots[i];
-      if (e.pid == 0) break;
-      if (e.hash == h && e.len == n && memcmp(s.arena.data() + e.off, p, n) == 0) return e.pid;
-      i = (i + 1) & mask;
-    }
-    const int32_t pid = next_.fetch_add(1);
-    Slot ne{h, (uint32_t)s.arena.size(), (uint32_t)n, pid};
-    s.arena.append(p, n);
-    s.slots[i] = ne;
-    if (++s.used * 2 > s.slots.size()) grow(s);
-    return pid;
-  }
-  int32_t count() const { return next_.load() - 1; }
-  // all (string, provisional id)
-  void collect(std::vector<std::pair<std::string, int32_t>>& out) const {
-    for (const Stripe& s : stripes_)
-      for (const Slot& e : s.slots)
-        if (e.pid) out.emplace_back(std::string(s.arena.data() + e.off, e.len), e.pid);
-  }
-
- private:
-  struct Slot {
-    uint64_t hash;
-    uint32_t off, len;
-    int32_t pid;
-  };
-  struct Stripe {
-    std::mutex m;
-    std::vector<Slot> slots;
-    std::string arena;
-    size_t used = 0;
-  };
-  static void grow(Stripe& s) {
-    std::vector<Slot> old;
-    old.swap(s.slots);
-    s.slots.assign(old.size() * 2, Slot{0, 0, 0, 0});
-    const size_t mask = s.slots.size() - 1;
-    for (const Slot& e : old) {
-      if (!e.pid) continue;
-      size_t i = (e.hash >> 8) & mask;
-      while (s.slots[i].pid) i = (i + 1) & mask;
-      s.slots[i] = e;
-    }
-  }
-  Stripe stripes_[kStripes];
-  std::atomic<int32_t> next_;
-};
-
 // ---------------- records ----------------
 struct Columns {
   std::vector<int32_t> cell, umi, gene, ref, pos;
@@ -148,75 +64,6 @@ struct Columns {
     bits.resize(n), xf.resize(n), cy_gt30.resize(n), cy_len.resize(n), uy_gt30.resize(n), uy_len.resize(n);
   }
 };
-
-// a tag's value as the Python reader sees it: a string (Z, H, A; integers printed in decimal
-// for the string tags) or an integer
-struct TagVal {
-  bool present = false, is_str = false;
-  const char* s = nullptr;
-  size_t n = 0;
-  int64_t i = 0;
-  char num[24];
-};
-
-// Z/H/A/integer value at p (type t); returns the bytes the value occupies, or 0 for an
-// unknown type
-size_t read_tag(const uint8_t* p, const uint8_t* end, char t, TagVal* v) {
-  switch (t) {
-    case 'Z':
-    case 'H': {
-      const uint8_t* z = (const uint8_t*)memchr(p, 0, end - p);
-      if (!z) return 0;
-      if (v) v->present = true, v->is_str = true, v->s = (const char*)p, v->n = z - p;
-      return z - p + 1;
-    }
-    case 'A':
-      if (v) v->present = true, v->is_str = true, v->s = (const char*)p, v->n = 1;
-      return 1;
-    case 'c':
-      if (v) v->present = true, v->i = (int8_t)p[0];
-      return 1;
-    case 'C':
-      if (v) v->present = true, v->i = p[0];
-      return 1;
-    case 's':
-      if (v) v->present = true, v->i = (int16_t)rd16(p);
-      return 2;
-    case 'S':
-      if (v) v->present = true, v->i = rd16(p);
-      return 2;
-    case 'i':
-      if (v) v->present = true, v->i = (int32_t)rd32(p);
-      return 4;
-    case 'I':
-      if (v) v->present = true, v->i = rd32(p);
-      return 4;
-    case 'f':
-      if (v) v->present = true;
-      return 4;
-    case 'd':
-      if (v) v->present = true;
-      return 8;
-    case 'B': {
-      const char sub = (char)p[0];
-      const uint32_t cnt = rd32(p + 1);
-      const size_t w = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
-      if (v) v->present = true;
-      return 5 + (size_t)cnt * w;
-    }
-    default:
-      return 0;
-  }
-}
-
-// the string form of a value (the Python tag value passed through str())
-void as_str(TagVal& v) {
-  if (!v.present || v.is_str) return;
-  snprintf(v.num, sizeof(v.num), "%lld", (long long)v.i);
-  v.s = v.num;
-  v.n = strlen(v.num);
-  v.is_str = true;
-}
 
 bool str_eq(const TagVal& a, const TagVal& b) { return a.n == b.n && memcmp(a.s, b.s, a.n) == 0; }
 

@@ -8,6 +8,7 @@ codes as the reference's ``GenericPlatform`` metric commands
   CalculateGeneMetrics -i BAM -o STEM
   MergeCellMetrics FILES... -o STEM
   MergeGeneMetrics FILES... -o STEM
+  SplitBam -b BAM... -p PREFIX -t TAG... [-s MB] [--num-processes N] [--drop-missing]  (platform.py:153-223)
   CreateCountMatrix -b BAM -o PREFIX -a GTF [-c TAG -m TAG -g TAG -n]   (platform.py:384-470)
   MergeCountMatrices -i PREFIX... -o STEM                              (platform.py:475-516)
 
@@ -23,7 +24,7 @@ Run as ``python -m sctools_amd <Command> [args]``.
 import argparse
 from typing import Iterable, Set
 
-from sctools_amd import consts, count, gtf, metrics
+from sctools_amd import bam, consts, count, gtf, metrics
 
 
 def _engine_args(parser):
@@ -94,6 +95,29 @@ class GenericPlatform:
 
 
     @classmethod
+    def split_bam(cls, args: Iterable[str] = None) -> int:
+        """SplitBam (platform.py:153-223): prints the chunk file names, space-separated."""
+        parser = argparse.ArgumentParser()
+        parser.add_argument("-b", "--bamfile", nargs="+", required=True, help="input bamfile")
+        parser.add_argument("-p", "--output-prefix", required=True, help="prefix for output chunks")
+        parser.add_argument("-s", "--subfile-size", required=False, default=1000, type=float,
+                            help="approximate size target for each subfile (in MB)")
+        parser.add_argument("--num-processes", required=False, default=None, type=int,
+                            help="Number of processes to parallelize over")
+        parser.add_argument("-t", "--tags", nargs="+",
+                            help="tag(s) to split bamfile over. Tags are checked sequentially, and tags after the "
+                                 "first are only checked if the first tag is not present.")
+        parser.set_defaults(raise_missing=True)
+        parser.add_argument("--drop-missing", action="store_false",
+                            help="drop records without tag specified by -t/--tag (default behavior is to raise an "
+                                 "exception")
+        args = parser.parse_args(args) if args is not None else parser.parse_args()
+        filenames = bam.split(args.bamfile, args.output_prefix, args.tags, approx_mb_per_split=args.subfile_size,
+                              raise_missing=args.drop_missing, num_processes=args.num_processes)
+        print(" ".join(filenames))
+        return 0
+
+    @classmethod
     def bam_to_count_matrix(cls, args: Iterable[str] = None) -> int:
         """CreateCountMatrix (platform.py:384-470): query-name-grouped tagged BAM -> CSR count matrix."""
         parser = argparse.ArgumentParser()
@@ -146,6 +170,7 @@ COMMANDS = {
     "CalculateGeneMetrics": GenericPlatform.calculate_gene_metrics,
     "MergeCellMetrics": GenericPlatform.merge_cell_metrics,
     "MergeGeneMetrics": GenericPlatform.merge_gene_metrics,
+    "SplitBam": GenericPlatform.split_bam,
     "CreateCountMatrix": GenericPlatform.bam_to_count_matrix,
     "MergeCountMatrices": GenericPlatform.merge_count_matrices,
 }
