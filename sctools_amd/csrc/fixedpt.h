@@ -58,11 +58,13 @@ SCT_HD uint64_t dbits(double x) {
 #endif
 }
 
-// Add X = x*2^68 and X^2 into 8 lanes (limb sums).  x must be 0 or in [2^-16, 2^16).
+// The 8 lane increments of one sample x (fx_accumulate adds exactly these): X = x*2^68 and X^2
+// as 32-bit limb pieces.  x must be 0 or in [2^-16, 2^16).  inc[7] (bits >= 128 of X^2) is
+// returned as 64 bits: it exceeds 32 bits only for x >= 2^12.
 // The 53-bit significand is split as m = mh 2^32 + ml (mh < 2^21), so m^2 takes three 32x32
 // products instead of a general 64x64 multiply, and the shifts by s and 2s use the
 // (v >> 1) >> (63 - k) form, which needs no select for k == 0.
-SCT_HD void fx_accumulate(int64_t* lanes, double x) {
+SCT_HD void fx_increments(double x, uint32_t (&inc)[kStreamLanes - 1], uint64_t& inc7) {
   const uint64_t b = dbits(x);
   const uint32_t bhi = (uint32_t)(b >> 32);
   const int ex = (int)((bhi >> 20) & 0x7ff);
@@ -73,9 +75,9 @@ SCT_HD void fx_accumulate(int64_t* lanes, double x) {
   const uint64_t m = ((uint64_t)mh << 32) | ml;
   const uint64_t lo = m << s;
   const uint32_t hi = (uint32_t)(((uint64_t)mh << s) >> 32);
-  lanes[0] += (int64_t)(lo & 0xffffffffu);
-  lanes[1] += (int64_t)(lo >> 32);
-  lanes[2] += (int64_t)hi;
+  inc[0] = (uint32_t)lo;
+  inc[1] = (uint32_t)(lo >> 32);
+  inc[2] = hi;
   // m^2 = A + 2B 2^32 + C 2^64
   const uint64_t A = (uint64_t)ml * ml;
   const uint64_t B2 = ((uint64_t)ml * mh) << 1;  // < 2^54
@@ -86,11 +88,20 @@ SCT_HD void fx_accumulate(int64_t* lanes, double x) {
   const uint64_t w0 = plo << t;
   const uint64_t w1 = (phi << t) | ((plo >> 1) >> (63 - t));
   const uint64_t w2 = (phi >> 1) >> (63 - t);
-  lanes[3] += (int64_t)(w0 & 0xffffffffu);
-  lanes[4] += (int64_t)(w0 >> 32);
-  lanes[5] += (int64_t)(w1 & 0xffffffffu);
-  lanes[6] += (int64_t)(w1 >> 32);
-  lanes[7] += (int64_t)w2;
+  inc[3] = (uint32_t)w0;
+  inc[4] = (uint32_t)(w0 >> 32);
+  inc[5] = (uint32_t)w1;
+  inc[6] = (uint32_t)(w1 >> 32);
+  inc7 = w2;
+}
+
+// Add X = x*2^68 and X^2 into 8 lanes (limb sums).  x must be 0 or in [2^-16, 2^16).
+SCT_HD void fx_accumulate(int64_t* lanes, double x) {
+  uint32_t inc[kStreamLanes - 1];
+  uint64_t inc7;
+  fx_increments(x, inc, inc7);
+  for (int k = 0; k < kStreamLanes - 1; k++) lanes[k] += (int64_t)inc[k];
+  lanes[kStreamLanes - 1] += (int64_t)inc7;
 }
 
 // ---- small fixed-size unsigned big integers (little-endian 64-bit limbs) ----
