@@ -251,7 +251,8 @@ int sct_tag_sort_workspace_size(const sct_plan_t* plan, size_t* bytes);
  * the sorted tag strings, a missing tag first, as bam.get_tag_or_default(..., "")
  * sorts), then by `tiebreak` (nullable device int32 ids in [0, n_tiebreak_ids):
  * the query-name rank).  Without a tiebreak, ties keep input order (Python's
- * sorted() is stable).  Does not synchronize. */
+ * sorted() is stable).  Does not synchronize without a tiebreak; with one it synchronizes
+ * `stream` once (to size the tiebreak pass over runs of equal tag fields). */
 int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t* tiebreak,
                  int32_t n_tiebreak_ids, int32_t order, const sct_records_t* out, void* workspace,
                  size_t workspace_bytes, void* stream);

@@ -13,7 +13,10 @@
 namespace sct {
 
 constexpr int kItems = 16;
-constexpr int kTile = kBlock * kItems;  // 4096 records per tile
+constexpr int kTile = kBlock * kItems;  // 4096 records per tile (entity-run heads, key pass)
+// LSD radix sort tiles: 2048 items (24 KB of keys / values staged in LDS, so 6 blocks fit a CU)
+constexpr int kSortItems = 8;
+constexpr int kSortTile = kBlock * kSortItems;
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
 static_assert(kRadix == kBlock, "digit-per-thread scan assumes kRadix == kBlock");
@@ -24,9 +27,9 @@ __global__ void k_radix_upsweep(const uint64_t* __restrict__ keys, int64_t n, in
   const int wid = threadIdx.x / kWave;
   for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&hist[0][0])[i] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kTile;
-#pragma unroll 4
-  for (int j = 0; j < kItems; j++) {
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+#pragma unroll
+  for (int j = 0; j < kSortItems; j++) {
     const int64_t p = base + (int64_t)j * kBlock + threadIdx.x;
     if (p < n) atomicAdd(&hist[wid][(keys[p] >> shift) & (kRadix - 1)], 1u);
   }
@@ -44,29 +47,31 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __re
                                                             uint64_t* __restrict__ keys_out,
                                                             uint32_t* __restrict__ vals_out, int64_t n, int shift,
                                                             int64_t num_tiles, const uint32_t* __restrict__ offsets) {
-  __shared__ uint64_t s_keys[kTile];
-  __shared__ uint32_t s_vals[kTile];
+  __shared__ uint64_t s_keys[kSortTile];
+  __shared__ uint32_t s_vals[kSortTile];
   __shared__ uint32_t s_whist[kWaves][kRadix];
   __shared__ uint32_t s_dstart[kRadix];
+  __shared__ uint32_t s_goff[kRadix];  // this tile's output offset per digit (one global read each)
   __shared__ uint64_t s_scan[kWaves + 1];
 
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
-  const int64_t base = (int64_t)blockIdx.x * kTile;
-  const int tile_n = (int)((n - base) < kTile ? (n - base) : kTile);
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  const int tile_n = (int)((n - base) < kSortTile ? (n - base) : kSortTile);
 
   for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_whist[0][0])[i] = 0;
+  s_goff[threadIdx.x] = offsets[(int64_t)threadIdx.x * num_tiles + blockIdx.x];  // kRadix == kBlock
   __syncthreads();
 
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  uint64_t k[kItems];
-  uint32_t v[kItems];
-  uint16_t rank[kItems];
-  uint8_t dig[kItems];
-  // wave `wid` owns tile positions [wid*kItems*kWave, (wid+1)*kItems*kWave); round j covers 64 of them
+  uint64_t k[kSortItems];
+  uint32_t v[kSortItems];
+  uint16_t rank[kSortItems];
+  uint8_t dig[kSortItems];
+  // wave `wid` owns tile positions [wid*kSortItems*kWave, ...); round j covers 64 of them
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
-    const int q = wid * (kItems * kWave) + j * kWave + lane;
+  for (int j = 0; j < kSortItems; j++) {
+    const int q = wid * (kSortItems * kWave) + j * kWave + lane;
     const int64_t p = base + q;
     if (q < tile_n) {
       k[j] = keys_in[p];
@@ -111,7 +116,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __re
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
+  for (int j = 0; j < kSortItems; j++) {
     const uint32_t lp = s_whist[wid][dig[j]] + rank[j];
     s_keys[lp] = k[j];
     s_vals[lp] = v[j];
@@ -120,7 +125,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __re
   for (int q = threadIdx.x; q < tile_n; q += kBlock) {
     const uint64_t kk = s_keys[q];
     const uint32_t d = (uint32_t)(kk >> shift) & (kRadix - 1);
-    const uint64_t o = (uint64_t)offsets[(int64_t)d * num_tiles + blockIdx.x] + (uint32_t)(q - (int)s_dstart[d]);
+    const uint64_t o = (uint64_t)s_goff[d] + (uint32_t)(q - (int)s_dstart[d]);
     keys_out[o] = kk;
     vals_out[o] = s_vals[q];
   }
@@ -129,14 +134,14 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __re
 struct SortBuffers {
   uint64_t *ka, *kb;
   uint32_t *va, *vb;
-  uint32_t *counts, *offsets;  // kRadix * cdiv(n, kTile) each
+  uint32_t *counts, *offsets;  // kRadix * cdiv(n, kSortTile) each
   uint64_t* sums;              // cdiv(kRadix * tiles, kScanChunk)
 };
 
 // LSD sort of (ka, va) over the low `bits` bits; *which = 0 if the result is in (ka, va), 1 if in (kb, vb)
 inline int radix_sort(const SortBuffers& B, int64_t n, int bits, int* which, hipStream_t s) {
   const int passes = (bits + kRadixBits - 1) / kRadixBits;
-  const int64_t tiles = cdiv(n, kTile);
+  const int64_t tiles = cdiv(n, kSortTile);
   int cur = 0;
   for (int ps = 0; ps < passes; ps++) {
     const int shift = ps * kRadixBits;

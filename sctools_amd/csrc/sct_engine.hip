@@ -56,7 +56,7 @@ Layout layout_for(const sct_plan_t* plan) {
   const int64_t n = plan->n_records > 0 ? plan->n_records : 0;
   const int64_t n1 = n > 0 ? n : 1;
   L.num_tiles = cdiv(n1, kTile);
-  const int64_t m = (int64_t)kRadix * L.num_tiles;
+  const int64_t m = (int64_t)kRadix * cdiv(n1, kSortTile);  // radix counts of the global-sort path
   L.num_chunks = cdiv(m, kScanChunk);
   L.max_ent = plan->max_entities > 0 ? plan->max_entities : n1;
   L.gene = plan->mode == SCT_MODE_GENE_GROUPED || (plan->flags & SCT_PLAN_GENE_PARTIALS);
@@ -473,7 +473,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
 
 // ---- tag sort ----
 struct SortLayout {
-  size_t recs, recs2, ka, kb, va, vb, counts, offsets, sums, bad, total;
+  size_t recs, recs2, ka, kb, va, vb, counts, offsets, sums, bad, lka, lkb, lva, lvb, longs, tctl, total;
 };
 
 struct CountLayout {
@@ -486,7 +486,7 @@ CountLayout count_layout(const sct_count_input_t* in) {
   const int64_t n1 = in->n > 0 ? in->n : 1;
   const int64_t c1 = in->n_cell_ids > 0 ? in->n_cell_ids : 1;
   const int64_t m = n1 > c1 ? n1 : c1;  // the record sort and the cell-order sort share buffers
-  const int64_t cm = (int64_t)kRadix * cdiv(m, kTile);
+  const int64_t cm = (int64_t)kRadix * cdiv(m, kSortTile);
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -538,6 +538,13 @@ SortLayout sort_layout(int64_t n) {
   L.offsets = take(sizeof(uint32_t) * (size_t)m);
   L.sums = take(sizeof(uint64_t) * (size_t)(cdiv(m, kScanChunk) + 1));
   L.bad = take(sizeof(uint64_t));
+  // tiebreak fix-up of runs longer than kTieShort (tagsort.h): compact keys / values, run list
+  L.lka = take(sizeof(uint64_t) * (size_t)n1);
+  L.lkb = take(sizeof(uint64_t) * (size_t)n1);
+  L.lva = take(sizeof(uint32_t) * (size_t)n1);
+  L.lvb = take(sizeof(uint32_t) * (size_t)n1);
+  L.longs = take(sizeof(uint4) * (size_t)(n1 / (kTieShort + 1) + 1));
+  L.tctl = take(2 * sizeof(uint32_t));
   L.total = off;
   return L;
 }
@@ -772,6 +779,42 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
                 at<uint64_t>(workspace, L.sums)};
   const dim3 grid((unsigned)cdiv(n, kBlock));
   LAUNCH("tag_pack", k_pack, grid, dim3(kBlock), s, *in, recs);
+  int field_bits = 0;
+  for (int i = 0; i < nf - (tiebreak ? 1 : 0); i++) field_bits += f[i].bits;
+  if (tiebreak && field_bits <= 64) {
+    // one radix sort on the tag fields, then the query-name order inside runs of equal fields
+    RoundKey rk{};
+    rk.nf = nf - 1;
+    rk.bits = field_bits;
+    for (int i = 0; i < rk.nf; i++) rk.f[i] = f[i];
+    LAUNCH("tag_keys", k_field_keys, grid, dim3(kBlock), s, *in, n, rk, B.ka, B.va);
+    int which = 0;
+    rc = radix_sort(B, n, field_bits, &which, s);
+    if (rc) return rc;
+    const uint64_t* keys = which ? B.kb : B.ka;
+    uint32_t* perm = which ? B.vb : B.va;
+    uint4* longs = at<uint4>(workspace, L.longs);
+    uint32_t* tctl = at<uint32_t>(workspace, L.tctl);
+    HIPCHK(hipMemsetAsync(tctl, 0, 2 * sizeof(uint32_t), s));
+    uint32_t* pos_of = at<uint32_t>(workspace, L.recs2);  // the row buffer is free on this path
+    LAUNCH("tag_ties", k_tie_wave, grid, dim3(kBlock), s, keys, perm, tiebreak, n, longs, tctl);
+    uint32_t h[2] = {0, 0};
+    if (int rb = readback(h, tctl, sizeof(h), s)) return rb;
+    if (h[0] > 0) {  // runs longer than kTieShort: (run, tiebreak) radix sort of their records
+      const int tie_bits = bitlen((uint64_t)n_tiebreak_ids);
+      SortBuffers LB{at<uint64_t>(workspace, L.lka), at<uint64_t>(workspace, L.lkb), at<uint32_t>(workspace, L.lva),
+                     at<uint32_t>(workspace, L.lvb), B.counts, B.offsets, B.sums};
+      LAUNCH("tag_long_keys", k_long_keys, dim3(h[0]), dim3(kBlock), s, (const uint4*)longs, (const uint32_t*)perm,
+             tiebreak, tie_bits, LB.ka, LB.va, pos_of);
+      int w2 = 0;
+      rc = radix_sort(LB, (int64_t)h[1], bitlen((uint64_t)h[1]) + tie_bits, &w2, s);
+      if (rc) return rc;
+      LAUNCH("tag_long_scatter", k_long_scatter, dim3((unsigned)cdiv(h[1], kBlock)), dim3(kBlock), s,
+             (const uint32_t*)pos_of, (const uint32_t*)(w2 ? LB.vb : LB.va), (int64_t)h[1], perm);
+    }
+    LAUNCH("tag_unpack", k_unpack, grid, dim3(kBlock), s, (const uint4*)recs, (const uint32_t*)perm, n, *out);
+    return SCT_OK;
+  }
   // rounds: fields from the least significant end, packed greedily into <= 64-bit keys
   const uint32_t* perm = nullptr;
   int hi = nf;  // fields [lo, hi) of the next round (most significant first)

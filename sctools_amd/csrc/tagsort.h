@@ -150,12 +150,14 @@ __global__ void __launch_bounds__(kBlock) k_row_scatter(sct_records_t in, const 
   __shared__ uint4 s_rows[2 * kRowTile];
   __shared__ uint32_t s_whist[kWaves][kRadix];
   __shared__ uint32_t s_dstart[kRadix];
+  __shared__ uint32_t s_goff[kRadix];
   __shared__ uint64_t s_scan[kWaves + 1];
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
   const int64_t base = (int64_t)blockIdx.x * kRowTile;
   const int tile_n = (int)((n - base) < kRowTile ? (n - base) : kRowTile);
   for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_whist[0][0])[i] = 0;
+  s_goff[threadIdx.x] = offsets[(int64_t)threadIdx.x * tiles + blockIdx.x];
   __syncthreads();
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
   uint4 ra[kRowItems], rb[kRowItems];
@@ -228,7 +230,7 @@ __global__ void __launch_bounds__(kBlock) k_row_scatter(sct_records_t in, const 
     const uint4 a = s_rows[2 * q];
     const uint4 b = s_rows[2 * q + 1];
     const uint32_t d = (a.x >> shift) & (kRadix - 1);
-    const uint64_t o = (uint64_t)offsets[(int64_t)d * tiles + blockIdx.x] + (uint32_t)(q - (int)s_dstart[d]);
+    const uint64_t o = (uint64_t)s_goff[d] + (uint32_t)(q - (int)s_dstart[d]);
     if constexpr (kToSoA) {
       const_cast<int32_t*>(out.cell)[o] = (int32_t)a.x;
       const_cast<int32_t*>(out.umi)[o] = (int32_t)a.y;
@@ -250,6 +252,158 @@ __global__ void __launch_bounds__(kBlock) k_row_scatter(sct_records_t in, const 
       key_out[o] = (int32_t)a.x;
     }
   }
+}
+
+
+// ---- orders whose fields fit one 64-bit key, with a tiebreak (TagSortBam: CB, UB, GE, query name) ----
+// One LSD radix sort of (fields key, record index) from the SoA columns, then the tiebreak inside
+// each run of equal keys (molecules, mostly a few records): runs of <= kTieShort records are
+// sorted by one thread with a sorting network on (tiebreak, index) -- the index is increasing in
+// a run (the sort is stable), so ties keep input order as sorted() does; longer runs are gathered
+// into a compact list and radix-sorted by (run, tiebreak).  This replaces a second full radix
+// round (27 query-name bits) and the gather of its keys.
+constexpr int kTieShort = 16;
+
+__global__ void __launch_bounds__(kBlock) k_field_keys(sct_records_t r, int64_t n, RoundKey rk,
+                                                       uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t f[3] = {(uint32_t)r.cell[j], (uint32_t)r.umi[j], (uint32_t)r.gene[j]};
+  uint64_t k = 0;
+  for (int i = 0; i < rk.nf; i++) {
+    const int b = rk.f[i].bits;
+    const uint64_t v = (uint64_t)f[rk.f[i].which] & (b >= 32 ? 0xFFFFFFFFull : ((1ull << b) - 1));
+    k = b ? ((b >= 64 ? 0ull : (k << b)) | v) : k;
+  }
+  keys[j] = k;
+  vals[j] = (uint32_t)j;
+}
+
+__device__ __forceinline__ void ce(uint64_t& a, uint64_t& b) {
+  const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+  a = lo;
+  b = hi;
+}
+
+// Batcher's odd-even merge sort on 16
+constexpr int kNet16[63][2] = {
+    {0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}, {4, 5}, {6, 7}, {4, 6}, {5, 7}, {5, 6}, {0, 4}, {2, 6}, {2, 4},
+    {1, 5}, {3, 7}, {3, 5}, {1, 2}, {3, 4}, {5, 6}, {8, 9}, {10, 11}, {8, 10}, {9, 11}, {9, 10}, {12, 13},
+    {14, 15}, {12, 14}, {13, 15}, {13, 14}, {8, 12}, {10, 14}, {10, 12}, {9, 13}, {11, 15}, {11, 13}, {9, 10},
+    {11, 12}, {13, 14}, {0, 8}, {4, 12}, {4, 8}, {2, 10}, {6, 14}, {6, 10}, {2, 4}, {6, 8}, {10, 12}, {1, 9},
+    {5, 13}, {5, 9}, {3, 11}, {7, 15}, {7, 11}, {3, 5}, {7, 9}, {11, 13}, {1, 2}, {3, 4}, {5, 6}, {7, 8},
+    {9, 10}, {11, 12}, {13, 14}};
+
+// The tiebreak inside every run of >= 2 equal keys, one wave per 64 sorted positions:
+//   * runs that lie inside the wave's positions are sorted all at once by a 64-lane bitonic network
+//     on (run start lane, tiebreak, lane) -- the lane is the input order inside a run (the radix
+//     sort is stable), so ties of equal names keep it, as sorted() does; other lanes key on their
+//     own lane and stay put;
+//   * the run that crosses the wave's end is finished by its first lane (serially: <= kTieShort
+//     records in registers, longer runs to the compact list, ctl[0] runs / ctl[1] records);
+//     the lanes of a run that started in an earlier wave belong to that wave.
+// The tiebreak gather (random) is issued only for lanes in runs of >= 2.
+__device__ __forceinline__ void tie_serial(const uint64_t* __restrict__ keys, uint32_t* __restrict__ perm,
+                                           const int32_t* __restrict__ tie, int64_t n, int64_t p,
+                                           uint4* __restrict__ longs, uint32_t* __restrict__ ctl) {
+  const uint64_t k = keys[p];
+  int L = 1;
+  while (L <= kTieShort && p + L < n && keys[p + L] == k) L++;
+  if (L == 1) return;
+  if (L > kTieShort) {
+    int64_t e = p + L;
+    while (e < n && keys[e] == k) e++;
+    const uint32_t len = (uint32_t)(e - p);
+    const uint32_t slot = atomicAdd(&ctl[0], 1u);
+    const uint32_t off = atomicAdd(&ctl[1], len);
+    longs[slot] = make_uint4((uint32_t)p, len, off, 0u);
+    return;
+  }
+  uint64_t v[kTieShort];
+#pragma unroll
+  for (int i = 0; i < kTieShort; i++) {
+    if (i < L) {
+      const uint32_t idx = perm[p + i];
+      v[i] = ((uint64_t)(uint32_t)tie[idx] << 32) | idx;
+    } else {
+      v[i] = ~0ull;  // sentinel: sorts last
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 63; c++) ce(v[kNet16[c][0]], v[kNet16[c][1]]);
+#pragma unroll
+  for (int i = 0; i < kTieShort; i++)
+    if (i < L) perm[p + i] = (uint32_t)v[i];
+}
+
+__global__ void __launch_bounds__(kBlock) k_tie_wave(const uint64_t* __restrict__ keys, uint32_t* __restrict__ perm,
+                                                     const int32_t* __restrict__ tie, int64_t n,
+                                                     uint4* __restrict__ longs, uint32_t* __restrict__ ctl) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = p < n;
+  const uint64_t k = valid ? keys[p] : 0ull;
+  uint64_t kp = __shfl_up(k, 1), kn = __shfl_down(k, 1);
+  if (lane == 0) kp = (p > 0 && valid) ? keys[p - 1] : ~k;
+  if (lane == kWave - 1) kn = (p + 1 < n) ? keys[p + 1] : ~k;
+  const bool head = !valid || k != kp;
+  const bool tail = !valid || p + 1 >= n || k != kn;
+  const uint64_t H = __ballot(head), T = __ballot(tail);
+  const uint64_t upto = lane == kWave - 1 ? ~0ull : ((2ull << lane) - 1);
+  const uint64_t from = ~((1ull << lane) - 1);
+  const uint64_t hs = H & upto, ts = T & from;
+  const int s0 = hs ? 63 - __clzll((long long)hs) : -1;  // first lane of the lane's run, if in this wave
+  const int s1 = ts ? __ffsll((unsigned long long)ts) - 1 : -1;  // last lane of the run, if in this wave
+  const bool need = valid && s0 >= 0 && s1 >= 0 && s1 > s0;
+  uint32_t idx = valid ? perm[p] : 0u;
+  if (__ballot(need)) {
+    const uint32_t t = need ? (uint32_t)tie[idx] : 0u;
+    uint64_t key = ((uint64_t)(need ? s0 : lane) << 58) | ((uint64_t)t << 6) | (uint64_t)lane;
+#pragma unroll
+    for (int size = 2; size <= kWave; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const uint64_t ok = __shfl_xor(key, stride);
+        const uint32_t ov = (uint32_t)__shfl_xor((int)idx, stride);
+        const bool asc = (lane & size) == 0 || size == kWave;
+        const bool low = (lane & stride) == 0;
+        const bool take = (low == asc) ? (ok < key) : (ok > key);
+        key = take ? ok : key;
+        idx = take ? ov : idx;
+      }
+    }
+    if (need) perm[p] = idx;
+  }
+  // the run crossing the wave's end: its first lane (in this wave) sorts all of it
+  if (!((T >> (kWave - 1)) & 1ull)) {
+    const int h = H ? 63 - __clzll((long long)H) : -1;
+    if (h >= 0 && lane == h) tie_serial(keys, perm, tie, n, p, longs, ctl);
+  }
+}
+
+// long runs, one block each: compact keys (compact offset of the run, tiebreak), values (record
+// index) and the position each compact slot maps back to.  Runs own disjoint compact ranges, so
+// sorted by (offset, tiebreak) every run's records stay inside its own range.
+__global__ void __launch_bounds__(kBlock) k_long_keys(const uint4* __restrict__ longs, const uint32_t* __restrict__ perm,
+                                                      const int32_t* __restrict__ tie, int tie_bits,
+                                                      uint64_t* __restrict__ ck, uint32_t* __restrict__ cv,
+                                                      uint32_t* __restrict__ pos_of) {
+  const uint4 L = longs[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < L.y; i += kBlock) {
+    const uint32_t idx = perm[L.x + i];
+    ck[L.z + i] = ((uint64_t)L.z << tie_bits) | (uint32_t)tie[idx];
+    cv[L.z + i] = idx;
+    pos_of[L.z + i] = L.x + i;
+  }
+}
+
+// the sorted compact list back into the runs' positions of `perm`
+__global__ void __launch_bounds__(kBlock) k_long_scatter(const uint32_t* __restrict__ pos_of,
+                                                         const uint32_t* __restrict__ cv, int64_t m,
+                                                         uint32_t* __restrict__ perm) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= m) return;
+  perm[pos_of[j]] = cv[j];
 }
 
 }  // namespace sct

@@ -198,3 +198,28 @@ def test_cell_order_row_passes(eng, n_cell_ids):
     idx = np_order(arrays, "cell")
     for c in N.RECORD_COLUMNS:
         assert np.array_equal(out[c], arrays[c][idx]), c
+
+
+@pytest.mark.gpu
+def test_tie_runs_of_every_length(eng):
+    """(CB, UB, GE) runs of 1 .. 5000 equal records with random query names: the short runs are
+    ordered by the in-register network, the long ones (> 16) by the compact (run, name) sort --
+    both must give numpy's stable lexsort, ties of equal names in input order."""
+    from sctools_amd import engine as E
+
+    d, _, arrays = shuffled_synth(60_000, 11, n_cells=50)
+    arrays = {c: a.copy() for c, a in arrays.items()}
+    rng = np.random.default_rng(4)
+    start = 0
+    for L in [2, 3, 4, 5, 8, 9, 15, 16, 17, 31, 64, 300, 5000]:
+        idx = rng.choice(arrays["cell"].shape[0], size=L, replace=False)
+        for c in ("cell", "umi", "gene"):
+            arrays[c][idx] = arrays[c][idx[0]]
+        start += L
+    n = arrays["cell"].shape[0]
+    tie = rng.integers(0, 40, n).astype(np.int32)  # few names: equal names inside runs too
+    dims = E.Dims(d.n_cell_ids, d.n_gene_ids, d.n_umi_ids)
+    out = to_host(eng.tag_sort(to_dev(eng, arrays), dims, "cell_umi_gene", torch.from_numpy(tie).to(eng.device), 40))
+    idx = np_order(arrays, "cell_umi_gene", tie)
+    for c in N.RECORD_COLUMNS:
+        assert np.array_equal(out[c], arrays[c][idx]), c
