@@ -254,18 +254,20 @@ __global__ void __launch_bounds__(kBlock) k_gene_plan(const uint32_t* __restrict
 __device__ __forceinline__ uint32_t gswz(uint32_t i) { return i ^ ((i >> 3) & 7u); }
 static_assert(kGeneItems == 8, "gswz assumes 8 payloads per thread");
 
-// Bit i of an 8-bit value moved to bit 4i (nibble i) of a 32-bit word.
-__device__ __forceinline__ uint32_t spread_nibbles(uint32_t x) {
-  x = (x | (x << 12)) & 0x000F000Fu;
-  x = (x | (x << 6)) & 0x03030303u;
-  return (x | (x << 3)) & 0x11111111u;
+// Bit i of an 8-bit value moved to bit 8i (byte i) of a 64-bit word.
+__device__ __forceinline__ uint64_t spread_bytes(uint32_t x) {
+  uint64_t v = x;
+  v = (v | (v << 28)) & 0x0000000F0000000Full;
+  v = (v | (v << 14)) & 0x0003000300030003ull;
+  return (v | (v << 7)) & 0x0101010101010101ull;
 }
 
-// A thread's run of one gene.  The 16 flag bits are counted in nibbles of pk (a run collects at
-// most kGeneItems <= 15 payloads before it is flushed), two adds per payload instead of one
-// extract-and-add per flag; counts() expands them into the kGeneCnt counter lanes.
+// A thread's open run of one gene.  The 16 flag bits are counted in bytes of pk (a run stays
+// open over the sub-tiles of one work item: at most kGeneChunk / kGeneSub * kGeneItems
+// payloads), two 64-bit adds per payload instead of one extract-and-add per flag; counts()
+// expands them into the kGeneCnt counter lanes.
 struct GeneAcc {
-  uint32_t pk[2];  // nibble f of pk[f / 8]: #payloads with flag bit f
+  uint64_t pk[2];  // byte f of pk[f / 8]: #payloads with flag bit f
   int32_t n;       // n_reads
   int64_t l[3 * kStreamLanes];
   __device__ __forceinline__ void clear() {
@@ -276,8 +278,8 @@ struct GeneAcc {
   }
   __device__ __forceinline__ void add(const GenePayload& g, const double* s_rcp) {
     n += 1;
-    pk[0] += spread_nibbles(g.flags & 0xffu);
-    pk[1] += spread_nibbles((uint32_t)g.flags >> 8);
+    pk[0] += spread_bytes(g.flags & 0xffu);
+    pk[1] += spread_bytes((uint32_t)g.flags >> 8);
     fx_accumulate(l + 0 * kStreamLanes, ratio_rcp(g.uy_gt30, g.uy_len, s_rcp));
     fx_accumulate(l + 1 * kStreamLanes, ratio_rcp(g.gq_gt30, g.gq_len, s_rcp));
     fx_accumulate(l + 2 * kStreamLanes, ratio_rcp(g.gq_sum, g.gq_len, s_rcp));
@@ -287,9 +289,9 @@ struct GeneAcc {
   __device__ __forceinline__ void counts(int32_t (&c)[kGeneCnt]) const {
     c[0] = n;
 #pragma unroll
-    for (int f = 0; f < kGeneFlags; f++) c[1 + f] = (int32_t)((pk[f / 8] >> (4 * (f % 8))) & 0xfu);
-    c[1 + 9] -= (int32_t)((pk[1] >> 24) & 0xfu);
-    c[1 + 11] -= (int32_t)(pk[1] >> 28);
+    for (int f = 0; f < kGeneFlags; f++) c[1 + f] = (int32_t)((pk[f / 8] >> (8 * (f % 8))) & 0xffu);
+    c[1 + 9] -= (int32_t)((pk[1] >> 48) & 0xffu);
+    c[1 + 11] -= (int32_t)(pk[1] >> 56);
   }
   // unconditional adds (zeros included): a per-lane test would cost an exec-mask round per lane
   __device__ __forceinline__ void flush(int32_t* cbin, unsigned long long* lbin) const {
@@ -301,56 +303,80 @@ struct GeneAcc {
     for (int i = 0; i < 3 * kStreamLanes; i++) atomicAdd(&lbin[i], (unsigned long long)l[i]);
   }
 };
-static_assert(kGeneItems <= 15, "nibble counters");
+static_assert(kGeneChunk / kGeneSub * kGeneItems <= 255, "byte counters");
 static_assert(kGeneFlags == 14, "flag bits 14 and 15 are the SECOND events");
 
-// Segmented inclusive DPP scan of one value over the wave: lanes hold partial sums of the
-// segment (contiguous lanes with equal keys) that starts at lane `seg`; m[0..5] say whether
-// the source lane of each step (row_shr 1, 2, 4, 8; row_bcast 15; row_bcast 31) lies inside
-// the lane's segment.  Afterwards the last lane of every segment holds the segment's sum.
-template <typename T>
-__device__ __forceinline__ T seg_scan_dpp(T v, const bool (&m)[6]) {
-  T x;
-  x = dpp_val<0x111, 0xf>(v);  // row_shr:1
-  v += m[0] ? x : (T)0;
-  x = dpp_val<0x112, 0xf>(v);  // row_shr:2
-  v += m[1] ? x : (T)0;
-  x = dpp_val<0x114, 0xf>(v);  // row_shr:4
-  v += m[2] ? x : (T)0;
-  x = dpp_val<0x118, 0xf>(v);  // row_shr:8
-  v += m[3] ? x : (T)0;
-  x = dpp_val<0x142, 0xa>(v);  // row_bcast:15 (rows 1, 3 get lanes 15, 47)
-  v += m[4] ? x : (T)0;
-  x = dpp_val<0x143, 0xc>(v);  // row_bcast:31 (rows 2, 3 get lane 31)
-  v += m[5] ? x : (T)0;
-  return v;
+// Segmented inclusive DPP scan over the wave: lanes hold partial sums of the segment (adjacent
+// lanes with equal keys) that starts at lane `seg`.  Step j adds the value of the lane 1, 2, 4, 8
+// lanes back inside the row (row_shr), then of lane 15 of the previous row (row_bcast:15, rows 1
+// and 3) and of lane 31 (row_bcast:31, rows 2 and 3), where that lane lies in the segment
+// (m[j]); a step no lane needs is skipped (wave-uniform).  Afterwards the last lane of every
+// segment holds the segment's sum.  The DPP moves have no `old` operand: lanes whose source is
+// invalid are exactly the lanes with m[j] false.
+constexpr int kGenePack = 9;  // flag counts as 16-bit pairs (8 words) + n_reads
+
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_raw(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtrl, kRowMask, 0xf, false);
 }
 
-// Flush the wave's run accumulators: lanes hold runs of gene `key` (-1: none), equal keys in
-// contiguous lanes (the sub-tile is sorted and every thread owns consecutive payloads).  One
-// segmented scan per lane value, then the last lane of each segment adds its gene's sums to
-// the LDS bins -- one atomic per (segment, value) and no two lanes on one address, instead of
-// every lane adding its own run (up to 64 lanes on one bin).  Every lane must call it, all
-// active.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void seg_step(uint32_t (&c)[kGenePack], int64_t (&l)[3 * kStreamLanes], bool m) {
+#pragma unroll
+  for (int i = 0; i < kGenePack; i++) {
+    const uint32_t x = dpp_raw<kCtrl, kRowMask>(c[i]);
+    c[i] += m ? x : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < 3 * kStreamLanes; i++) {
+    const uint64_t v = (uint64_t)l[i];
+    const uint64_t x = ((uint64_t)dpp_raw<kCtrl, kRowMask>((uint32_t)(v >> 32)) << 32) |
+                       dpp_raw<kCtrl, kRowMask>((uint32_t)v);
+    l[i] += m ? (int64_t)x : 0;
+  }
+}
+
+// Flush the wave's run accumulators: lane runs of gene `key` (< 0: nothing to flush; the lane's
+// accumulator is left as it is).  Segments are maximal groups of adjacent lanes with one key;
+// after the segmented scan the last lane of each segment adds its gene's sums to the LDS bins --
+// one atomic per (segment, value), no two lanes on one address.  Every lane must call it, all
+// active; lanes with key >= 0 must clear their accumulator afterwards.
 __device__ __forceinline__ void gene_wave_flush(GeneAcc& acc, int key, int32_t* s_cbin, unsigned long long* s_lbin) {
   const int lane = threadIdx.x & (kWave - 1);
   const int prev = __shfl_up(key, 1);
   const uint64_t heads = __ballot(lane == 0 || prev != key);
   const uint64_t upto = lane == kWave - 1 ? ~0ull : ((1ull << (lane + 1)) - 1);
   const int seg = kWave - 1 - __clzll((unsigned long long)(heads & upto));
-  const bool m[6] = {seg <= lane - 1, seg <= lane - 2, seg <= lane - 4, seg <= lane - 8, seg < (lane & ~15), seg <= 31};
-  int32_t c[kGeneCnt];
-  acc.counts(c);
+  const int p = lane & 15;
+  const bool m0 = p >= 1 && seg <= lane - 1, m1 = p >= 2 && seg <= lane - 2;
+  const bool m2 = p >= 4 && seg <= lane - 4, m3 = p >= 8 && seg <= lane - 8;
+  const bool m4 = ((lane >> 4) & 1) && seg < (lane & ~15), m5 = lane >= 32 && seg <= 31;
+  // flag counts in 16-bit halves (a lane's run has < 256 payloads, a segment < 2^16)
+  uint32_t c[kGenePack];
 #pragma unroll
-  for (int i = 0; i < kGeneCnt; i++) c[i] = seg_scan_dpp(c[i], m);
-#pragma unroll
-  for (int i = 0; i < 3 * kStreamLanes; i++) acc.l[i] = seg_scan_dpp(acc.l[i], m);
+  for (int j = 0; j < 8; j++) {
+    const uint64_t w = acc.pk[j / 4] >> (16 * (j % 4));
+    c[j] = (uint32_t)(w & 0xffu) | ((uint32_t)((w >> 8) & 0xffu) << 16);
+  }
+  c[8] = (uint32_t)acc.n;
+  if (__ballot(m0)) seg_step<0x111, 0xf>(c, acc.l, m0);  // row_shr:1
+  if (__ballot(m1)) seg_step<0x112, 0xf>(c, acc.l, m1);  // row_shr:2
+  if (__ballot(m2)) seg_step<0x114, 0xf>(c, acc.l, m2);  // row_shr:4
+  if (__ballot(m3)) seg_step<0x118, 0xf>(c, acc.l, m3);  // row_shr:8
+  if (__ballot(m4)) seg_step<0x142, 0xa>(c, acc.l, m4);  // row_bcast:15
+  if (__ballot(m5)) seg_step<0x143, 0xc>(c, acc.l, m5);  // row_bcast:31
   const bool tail = lane == kWave - 1 || ((heads >> (lane + 1)) & 1ull);
   if (tail && key >= 0) {
     int32_t* cb = &s_cbin[key * kGeneCntPad];
     unsigned long long* lb = &s_lbin[key * 3 * kStreamLanes];
+    int32_t cnt[kGeneCnt];
+    cnt[0] = (int32_t)c[8];
 #pragma unroll
-    for (int i = 0; i < kGeneCnt; i++) atomicAdd(&cb[i], c[i]);
+    for (int f = 0; f < kGeneFlags; f++) cnt[1 + f] = (int32_t)((c[f / 2] >> (16 * (f % 2))) & 0xffffu);
+    cnt[1 + 9] -= (int32_t)(c[7] & 0xffffu);  // GF_MOL_SECOND (bit 14)
+    cnt[1 + 11] -= (int32_t)(c[7] >> 16);     // GF_FRAG_SECOND (bit 15)
+#pragma unroll
+    for (int i = 0; i < kGeneCnt; i++) atomicAdd(&cb[i], cnt[i]);
 #pragma unroll
     for (int i = 0; i < 3 * kStreamLanes; i++) atomicAdd(&lb[i], (unsigned long long)acc.l[i]);
   }
@@ -419,9 +445,21 @@ __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __res
       if (q < cnt) s_sorted[gswz(s_start[vx[j] - g0] + rk[j])] = src[sub + q];
     }
     __syncthreads();
-    // the thread's kGeneItems consecutive sorted payloads
+    // the thread's kGeneItems consecutive sorted payloads; its open run continues if they start
+    // with its gene, else the wave's changed runs are flushed together first
     const int j0 = t * kGeneItems;
     const int my_n = cnt - j0 < 0 ? 0 : (cnt - j0 < kGeneItems ? cnt - j0 : kGeneItems);
+    {
+      const int first = my_n > 0 ? (int)(s_sorted[gswz(j0)].x - g0) : cur;
+      const bool changed = cur >= 0 && first != cur;
+      if (__ballot(changed)) {
+        gene_wave_flush(acc, changed ? cur : -2 - (t & (kWave - 1)), s_cbin, s_lbin);
+        if (changed) {
+          acc.clear();
+          cur = -1;
+        }
+      }
+    }
     for (int k = 0; k < my_n; k++) {
       const uint4 w = s_sorted[gswz(j0 + k)];
       const GenePayload& g = *reinterpret_cast<const GenePayload*>(&w);
@@ -433,12 +471,12 @@ __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __res
       }
       acc.add(g, s_rcp);
     }
-    // the thread's last run joins its neighbours' runs of the same gene
-    gene_wave_flush(acc, cur, s_cbin, s_lbin);
-    acc.clear();
-    cur = -1;
+    // the thread's open run stays in registers: in a bucket's next sub-tile the thread's
+    // positions mostly hold the same gene again (sorted sub-tiles of the same gene mix)
     __syncthreads();  // s_sorted / s_cnt are reused by the next sub-tile
   }
+  // the threads' open runs, combined across each wave
+  gene_wave_flush(acc, cur, s_cbin, s_lbin);
   __syncthreads();
   // bins -> partial rows: counter lanes 0..14 are partial slots 0..14; stream lanes follow P_FLOAT
   for (int i = t; i < kGenesPerBucket * kGeneCnt; i += kBlock) {
