@@ -6,8 +6,9 @@
 // the cell-view sorted pass (reduce.h, DF_* flags by record index).  Here:
 //   k_gene_plan    bucket starts from the per-bucket record counts (build_keys) -> the
 //                  emit cursors and the reduce work list;
-//   k_gene_emit    input order, coalesced: one 16-byte GenePayload per record into its
-//                  gene bucket (kGenesPerBucket genes), one cursor atomic per (block, bucket);
+//   k_gene_emit    input order, coalesced: one payload per record into its gene bucket
+//                  (kGenesPerBucket genes), one cursor atomic per (block, bucket); 8 bytes
+//                  (gene_payload8) when the stream operands fit, else 16 (GenePayload);
 //   k_gene_reduce  each block counting-sorts sub-tiles of one bucket's payloads by gene in
 //                  LDS, sums each thread's runs of equal gene in registers, adds runs into
 //                  LDS bins, and the bins into the rows.
@@ -22,8 +23,7 @@
 namespace sct {
 
 constexpr int kGeneChunk = 16384;  // payloads per reduce block
-constexpr int kGeneSub = 2048;  // payloads sorted in LDS at a time
-constexpr int kGeneItems = kGeneSub / kBlock;
+constexpr int kGeneSub = 2048;  // 16-byte payloads sorted in LDS at a time (32 KB)
 constexpr int kGeneCnt = 1 + kGeneFlags;  // n_reads + flag counts (32-bit bins)
 constexpr int kGeneCntPad = 16;
 
@@ -50,9 +50,8 @@ __device__ __forceinline__ uint32_t block_rank(uint32_t key, int nbits, bool val
   return base + (uint32_t)__popcll(peers & lt);
 }
 
-// one 16-byte payload per record: everything GatherGeneMetrics derives from the record
-__device__ __forceinline__ uint4 gene_payload(uint32_t g, uint8_t bt, uint8_t xf, uint16_t df, uint8_t uy_gt30,
-                                              uint8_t uy_len, uint16_t gq_gt30, uint16_t gq_len, uint16_t gq_sum) {
+// the GF flags of one record: its own bits plus the distinct-count events of the cell view
+__device__ __forceinline__ uint32_t gene_flags(uint8_t bt, uint8_t xf, uint16_t df) {
   uint32_t f = (bt & SCT_B_PERFECT_UMI) ? GF_PERFECT_UMI : 0;
   if (!(bt & SCT_B_UNMAPPED)) {
     f |= (xf == SCT_XF_CODING ? GF_EXONIC : 0) | (xf == SCT_XF_INTRONIC ? GF_INTRONIC : 0) |
@@ -63,6 +62,12 @@ __device__ __forceinline__ uint4 gene_payload(uint32_t g, uint8_t bt, uint8_t xf
        (df & DF_FRAG_FIRST ? GF_FRAG_FIRST : 0) | (df & DF_FRAG_SINGLE ? GF_FRAG_SINGLE : 0) |
        (df & DF_K1_HEAD ? GF_CG_HEAD : 0) | (df & DF_K1_MULTI ? GF_CG_MULTI : 0) |
        (df & DF_MOL_SECOND ? GF_MOL_SECOND : 0) | (df & DF_FRAG_SECOND ? GF_FRAG_SECOND : 0);
+  return f;
+}
+
+// The wide payload: 16 bytes (GenePayload) -- everything GatherGeneMetrics derives from a record.
+__device__ __forceinline__ uint4 gene_payload(uint32_t g, uint32_t f, uint8_t uy_gt30, uint8_t uy_len,
+                                              uint16_t gq_gt30, uint16_t gq_len, uint16_t gq_sum) {
   GenePayload gp;
   gp.gene = g;
   gp.flags = (uint16_t)f;
@@ -73,6 +78,20 @@ __device__ __forceinline__ uint4 gene_payload(uint32_t g, uint8_t bt, uint8_t xf
   gp.gq_sum = gq_sum;
   gp.pad = 0;
   return *reinterpret_cast<const uint4*>(&gp);
+}
+
+// The narrow payload: the same in 8 bytes, used when every record's stream operands fit (the
+// exact-stream pass of build_keys checks them and sets *gwide otherwise; stream_tile):
+//   bits 0-5 the local gene (gene mod kGenesPerBucket: the bucket is the payload's region),
+//   6-20 the GF flags with EXONIC / INTRONIC / UTR (exclusive) as a 2-bit code (1, 2, 3),
+//   21-25 uy_gt30, 26-30 uy_len, 31-39 gq_gt30, 40-48 gq_len, 49-63 gq_sum.
+constexpr uint32_t kNarrowUy = 31, kNarrowGq = 511, kNarrowGqSum = 32767;
+__device__ __forceinline__ uint64_t gene_payload8(uint32_t g, uint32_t f, uint32_t uy_gt30, uint32_t uy_len,
+                                                  uint32_t gq_gt30, uint32_t gq_len, uint32_t gq_sum) {
+  const uint32_t code = ((f >> 1) & 1u) | ((f >> 1) & 2u) | ((f >> 3) & 1u) * 3u;
+  const uint32_t f15 = (f & 1u) | (code << 1) | ((f >> 4) << 3);
+  return (uint64_t)(g & (kGenesPerBucket - 1)) | ((uint64_t)f15 << 6) | ((uint64_t)uy_gt30 << 21) |
+         ((uint64_t)uy_len << 26) | ((uint64_t)gq_gt30 << 31) | ((uint64_t)gq_len << 40) | ((uint64_t)gq_sum << 49);
 }
 
 // kEmitVec consecutive elements of a column for one lane: one 4- to 16-byte load in a full
@@ -128,12 +147,11 @@ constexpr int kEmitBatch = 8;  // rounds whose gene loads are in flight together
 static_assert(kEmitTile <= 65536, "ranks are 16-bit");
 static_assert(kEmitRounds % kEmitBatch == 0, "whole batches");
 
-template <bool kFull>
+template <bool kFull, bool k8>
 __device__ __forceinline__ void gene_emit_tile(const int32_t* __restrict__ gene, const RecCols& r,
                                                const uint16_t* __restrict__ dflags, int64_t n, int64_t base,
-                                               uint32_t* __restrict__ cursor, int n_buckets,
-                                               GenePayload* __restrict__ pay, uint32_t* s_cnt, uint32_t* s_off,
-                                               uint16_t* s_rank) {
+                                               uint32_t* __restrict__ cursor, int n_buckets, void* __restrict__ pay,
+                                               uint32_t* s_cnt, uint32_t* s_off, uint16_t* s_rank) {
   const int t = threadIdx.x;
   int nbb = 0;
   while ((1 << nbb) < n_buckets) nbb++;
@@ -180,9 +198,14 @@ __device__ __forceinline__ void gene_emit_tile(const int32_t* __restrict__ gene,
     for (int k = 0; k < kEmitVec; k++) {
       if (kFull || p0 + k < n) {
         const uint32_t gk = (uint32_t)cur.g[k];
-        const uint4 w = gene_payload(gk, cur.bt[k], cur.xf[k], cur.df[k], cur.ug[k], cur.ul[k], cur.gg[k],
-                                     cur.gl[k], cur.gs[k]);
-        reinterpret_cast<uint4*>(pay)[(uint64_t)s_off[gk / kGenesPerBucket] + rk[k]] = w;
+        const uint32_t f = gene_flags(cur.bt[k], cur.xf[k], cur.df[k]);
+        const uint64_t at = (uint64_t)s_off[gk / kGenesPerBucket] + rk[k];
+        if constexpr (k8)
+          reinterpret_cast<uint64_t*>(pay)[at] = gene_payload8(gk, f, cur.ug[k], cur.ul[k], cur.gg[k], cur.gl[k],
+                                                               cur.gs[k]);
+        else
+          reinterpret_cast<uint4*>(pay)[at] = gene_payload(gk, f, cur.ug[k], cur.ul[k], cur.gg[k], cur.gl[k],
+                                                           cur.gs[k]);
       }
     }
     if (j + 1 < kEmitRounds) cur = nxt;
@@ -192,15 +215,19 @@ __device__ __forceinline__ void gene_emit_tile(const int32_t* __restrict__ gene,
 __global__ void __launch_bounds__(kBlock) k_gene_emit(const int32_t* __restrict__ gene, RecCols r,
                                                       const uint16_t* __restrict__ dflags, int64_t n,
                                                       uint32_t* __restrict__ cursor, int n_buckets,
-                                                      GenePayload* __restrict__ pay) {
+                                                      const uint32_t* __restrict__ gwide, void* __restrict__ pay) {
   uint32_t* s_cnt = sct_dyn_lds;              // n_buckets (dynamic LDS)
   uint32_t* s_off = sct_dyn_lds + n_buckets;  // n_buckets
   __shared__ __attribute__((aligned(16))) uint16_t s_rank[kEmitTile];
   const int64_t base = (int64_t)blockIdx.x * kEmitTile;
-  if (base + kEmitTile <= n)  // block-uniform
-    gene_emit_tile<true>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
-  else
-    gene_emit_tile<false>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
+  const bool full = base + kEmitTile <= n, wide = *gwide != 0;  // block-uniform
+  if (wide) {
+    if (full) gene_emit_tile<true, false>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
+    else gene_emit_tile<false, false>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
+  } else {
+    if (full) gene_emit_tile<true, true>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
+    else gene_emit_tile<false, true>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
+  }
 }
 
 // one block: bucket starts (exclusive scan of the bucket counts) -> the emit cursors and the
@@ -248,11 +275,66 @@ __global__ void __launch_bounds__(kBlock) k_gene_plan(const uint32_t* __restrict
   }
 }
 
-// s_sorted slot of sorted position i: within each group of 8 payloads (128 bytes) the slot is
-// XORed with the group index, so the 64 lanes reading their k-th payload (positions 8t + k)
-// spread over all 16-byte bank groups instead of 8-way conflicts.
-__device__ __forceinline__ uint32_t gswz(uint32_t i) { return i ^ ((i >> 3) & 7u); }
-static_assert(kGeneItems == 8, "gswz assumes 8 payloads per thread");
+// One payload as the reduction uses it: the local gene, the 16 counted flag bits and the three
+// stream operand pairs.
+struct GeneItem {
+  uint32_t lg, f, ua, ub, qa, qb, qs;
+};
+
+// The two payload formats.  kSub payloads of a sub-tile are sorted in the same 32 KB of LDS;
+// slot(i) is the LDS slot of sorted position i: within each 128-byte group of payloads the slot
+// is XORed with the group index, so the 64 lanes reading their k-th payload (thread t owns
+// positions kItems t .. kItems t + kItems - 1) spread over the banks.
+template <bool k8>
+struct GeneFmt;
+template <>
+struct GeneFmt<false> {  // GenePayload; counted flag bit f is GF bit f
+  using W = uint4;
+  static constexpr int kSub = 2048;
+  __device__ static uint32_t slot(uint32_t i) { return i ^ ((i >> 3) & 7u); }
+  __device__ static uint32_t local(const W* p, int q, uint32_t g0) {
+    return reinterpret_cast<const uint32_t*>(p)[4 * q] - g0;  // GenePayload.gene is the first word
+  }
+  __device__ static GeneItem item(const W& w, uint32_t g0) {
+    const GenePayload& g = *reinterpret_cast<const GenePayload*>(&w);
+    return GeneItem{g.gene - g0, g.flags, g.uy_gt30, g.uy_len, g.gq_gt30, g.gq_len, g.gq_sum};
+  }
+  template <typename B>
+  __device__ static void counts(B byte, int32_t n, int32_t (&c)[kGeneCnt]) {
+    c[0] = n;
+#pragma unroll
+    for (int f = 0; f < kGeneFlags; f++) c[1 + f] = byte(f);
+    c[1 + 9] -= byte(14);   // GF_MOL_SECOND
+    c[1 + 11] -= byte(15);  // GF_FRAG_SECOND
+  }
+};
+template <>
+struct GeneFmt<true> {  // gene_payload8; counted bits: 0 PERFECT, 1-2 the xf code, 3-14 GF 4-15, 15 UTR
+  using W = uint2;
+  static constexpr int kSub = 4096;
+  __device__ static uint32_t slot(uint32_t i) { return i ^ ((i >> 4) & 15u); }
+  __device__ static uint32_t local(const W* p, int q, uint32_t) {
+    return reinterpret_cast<const uint32_t*>(p)[2 * q] & (kGenesPerBucket - 1);
+  }
+  __device__ static GeneItem item(const W& w, uint32_t) {
+    const uint32_t f15 = (w.x >> 6) & 0x7fffu;
+    return GeneItem{w.x & (kGenesPerBucket - 1), f15 | (((f15 >> 1) & (f15 >> 2) & 1u) << 15), (w.x >> 21) & 31u,
+                    (w.x >> 26) & 31u, (w.x >> 31) | ((w.y & 0xffu) << 1), (w.y >> 8) & 511u, w.y >> 17};
+  }
+  template <typename B>
+  __device__ static void counts(B byte, int32_t n, int32_t (&c)[kGeneCnt]) {
+    c[0] = n;
+    c[1] = byte(0);              // GF_PERFECT_UMI
+    c[2] = byte(1) - byte(15);   // GF_EXONIC: code 1
+    c[3] = byte(2) - byte(15);   // GF_INTRONIC: code 2
+    c[4] = byte(15);             // GF_UTR: code 3
+#pragma unroll
+    for (int f = 4; f < kGeneFlags; f++) c[1 + f] = byte(f - 1);
+    c[1 + 9] -= byte(13);   // GF_MOL_SECOND
+    c[1 + 11] -= byte(14);  // GF_FRAG_SECOND
+  }
+};
+static_assert(kGeneFlags == 14, "flag bits 14 and 15 are the SECOND events");
 
 // Bit i of an 8-bit value moved to bit 8i (byte i) of a 64-bit word.
 __device__ __forceinline__ uint64_t spread_bytes(uint32_t x) {
@@ -262,12 +344,11 @@ __device__ __forceinline__ uint64_t spread_bytes(uint32_t x) {
   return (v | (v << 7)) & 0x0101010101010101ull;
 }
 
-// A thread's open run of one gene.  The 16 flag bits are counted in bytes of pk (a run stays
-// open over the sub-tiles of one work item: at most kGeneChunk / kGeneSub * kGeneItems
-// payloads), two 64-bit adds per payload instead of one extract-and-add per flag; counts()
-// expands them into the kGeneCnt counter lanes.
+// A thread's open run of one gene.  The 16 counted flag bits are counted in bytes of pk (a run
+// stays open over the sub-tiles of one work item: at most kGeneChunk / kSub * kItems payloads),
+// two 64-bit adds per payload instead of one extract-and-add per flag.
 struct GeneAcc {
-  uint64_t pk[2];  // byte f of pk[f / 8]: #payloads with flag bit f
+  uint64_t pk[2];  // byte f of pk[f / 8]: #payloads with counted bit f
   int32_t n;       // n_reads
   int64_t l[3 * kStreamLanes];
   __device__ __forceinline__ void clear() {
@@ -276,35 +357,28 @@ struct GeneAcc {
 #pragma unroll
     for (int i = 0; i < 3 * kStreamLanes; i++) l[i] = 0;
   }
-  __device__ __forceinline__ void add(const GenePayload& g, const double* s_rcp) {
+  __device__ __forceinline__ void add(const GeneItem& g, const double* s_rcp) {
     n += 1;
-    pk[0] += spread_bytes(g.flags & 0xffu);
-    pk[1] += spread_bytes((uint32_t)g.flags >> 8);
-    fx_accumulate(l + 0 * kStreamLanes, ratio_rcp(g.uy_gt30, g.uy_len, s_rcp));
-    fx_accumulate(l + 1 * kStreamLanes, ratio_rcp(g.gq_gt30, g.gq_len, s_rcp));
-    fx_accumulate(l + 2 * kStreamLanes, ratio_rcp(g.gq_sum, g.gq_len, s_rcp));
+    pk[0] += spread_bytes(g.f & 0xffu);
+    pk[1] += spread_bytes(g.f >> 8);
+    fx_accumulate(l + 0 * kStreamLanes, ratio_rcp(g.ua, g.ub, s_rcp));
+    fx_accumulate(l + 1 * kStreamLanes, ratio_rcp(g.qa, g.qb, s_rcp));
+    fx_accumulate(l + 2 * kStreamLanes, ratio_rcp(g.qs, g.qb, s_rcp));
   }
-  // counter lanes: n_reads, then flag f on lane 1 + f; GF_MOL_SECOND (bit 14) and GF_FRAG_SECOND
-  // (bit 15) subtract from the GF_MOL_SINGLE / GF_FRAG_SINGLE lanes
-  __device__ __forceinline__ void counts(int32_t (&c)[kGeneCnt]) const {
-    c[0] = n;
-#pragma unroll
-    for (int f = 0; f < kGeneFlags; f++) c[1 + f] = (int32_t)((pk[f / 8] >> (8 * (f % 8))) & 0xffu);
-    c[1 + 9] -= (int32_t)((pk[1] >> 48) & 0xffu);
-    c[1 + 11] -= (int32_t)(pk[1] >> 56);
-  }
+  __device__ __forceinline__ int32_t byte(int f) const { return (int32_t)((pk[f / 8] >> (8 * (f % 8))) & 0xffu); }
   // unconditional adds (zeros included): a per-lane test would cost an exec-mask round per lane
+  template <bool k8>
   __device__ __forceinline__ void flush(int32_t* cbin, unsigned long long* lbin) const {
     int32_t c[kGeneCnt];
-    counts(c);
+    GeneFmt<k8>::counts([this](int f) { return byte(f); }, n, c);
 #pragma unroll
     for (int i = 0; i < kGeneCnt; i++) atomicAdd(&cbin[i], c[i]);
 #pragma unroll
     for (int i = 0; i < 3 * kStreamLanes; i++) atomicAdd(&lbin[i], (unsigned long long)l[i]);
   }
 };
-static_assert(kGeneChunk / kGeneSub * kGeneItems <= 255, "byte counters");
-static_assert(kGeneFlags == 14, "flag bits 14 and 15 are the SECOND events");
+static_assert(kGeneChunk / GeneFmt<false>::kSub * (GeneFmt<false>::kSub / kBlock) <= 255, "byte counters");
+static_assert(kGeneChunk / GeneFmt<true>::kSub * (GeneFmt<true>::kSub / kBlock) <= 255, "byte counters");
 
 // Segmented inclusive DPP scan over the wave: lanes hold partial sums of the segment (adjacent
 // lanes with equal keys) that starts at lane `seg`.  Step j adds the value of the lane 1, 2, 4, 8
@@ -313,7 +387,7 @@ static_assert(kGeneFlags == 14, "flag bits 14 and 15 are the SECOND events");
 // (m[j]); a step no lane needs is skipped (wave-uniform).  Afterwards the last lane of every
 // segment holds the segment's sum.  The DPP moves have no `old` operand: lanes whose source is
 // invalid are exactly the lanes with m[j] false.
-constexpr int kGenePack = 9;  // flag counts as 16-bit pairs (8 words) + n_reads
+constexpr int kGenePack = 9;  // counted flags as 16-bit pairs (8 words) + n_reads
 
 template <int kCtrl, int kRowMask>
 __device__ __forceinline__ uint32_t dpp_raw(uint32_t v) {
@@ -341,6 +415,7 @@ __device__ __forceinline__ void seg_step(uint32_t (&c)[kGenePack], int64_t (&l)[
 // after the segmented scan the last lane of each segment adds its gene's sums to the LDS bins --
 // one atomic per (segment, value), no two lanes on one address.  Every lane must call it, all
 // active; lanes with key >= 0 must clear their accumulator afterwards.
+template <bool k8>
 __device__ __forceinline__ void gene_wave_flush(GeneAcc& acc, int key, int32_t* s_cbin, unsigned long long* s_lbin) {
   const int lane = threadIdx.x & (kWave - 1);
   const int prev = __shfl_up(key, 1);
@@ -351,7 +426,7 @@ __device__ __forceinline__ void gene_wave_flush(GeneAcc& acc, int key, int32_t* 
   const bool m0 = p >= 1 && seg <= lane - 1, m1 = p >= 2 && seg <= lane - 2;
   const bool m2 = p >= 4 && seg <= lane - 4, m3 = p >= 8 && seg <= lane - 8;
   const bool m4 = ((lane >> 4) & 1) && seg < (lane & ~15), m5 = lane >= 32 && seg <= 31;
-  // flag counts in 16-bit halves (a lane's run has < 256 payloads, a segment < 2^16)
+  // counted flags in 16-bit halves (a lane's run has < 256 payloads, a segment < 2^16)
   uint32_t c[kGenePack];
 #pragma unroll
   for (int j = 0; j < 8; j++) {
@@ -370,11 +445,8 @@ __device__ __forceinline__ void gene_wave_flush(GeneAcc& acc, int key, int32_t* 
     int32_t* cb = &s_cbin[key * kGeneCntPad];
     unsigned long long* lb = &s_lbin[key * 3 * kStreamLanes];
     int32_t cnt[kGeneCnt];
-    cnt[0] = (int32_t)c[8];
-#pragma unroll
-    for (int f = 0; f < kGeneFlags; f++) cnt[1 + f] = (int32_t)((c[f / 2] >> (16 * (f % 2))) & 0xffffu);
-    cnt[1 + 9] -= (int32_t)(c[7] & 0xffffu);  // GF_MOL_SECOND (bit 14)
-    cnt[1 + 11] -= (int32_t)(c[7] >> 16);     // GF_FRAG_SECOND (bit 15)
+    GeneFmt<k8>::counts([&c](int f) { return (int32_t)((c[f / 2] >> (16 * (f % 2))) & 0xffffu); }, (int32_t)c[8],
+                        cnt);
 #pragma unroll
     for (int i = 0; i < kGeneCnt; i++) atomicAdd(&cb[i], cnt[i]);
 #pragma unroll
@@ -382,17 +454,98 @@ __device__ __forceinline__ void gene_wave_flush(GeneAcc& acc, int key, int32_t* 
   }
 }
 
-// One work item = (gene bucket, range of its payloads).  Each sub-tile of kGeneSub payloads is
-// counting-sorted in LDS by local gene id, so every thread's kGeneItems consecutive payloads are
-// long runs of one gene: registers accumulate a run; a run that ends inside the thread's
-// payloads goes to the LDS bins directly, and the runs still open at the end of the sub-tile
-// are combined across the wave by a segmented DPP scan (gene_wave_flush), so one lane per
-// gene per wave adds the 39 lanes (15 counters, 24 exact-sum lanes) to the bins.
-__global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __restrict__ pay,
-                                                        const int64_t* __restrict__ work,
+// One work item = (gene bucket, range [beg, end) of its payloads).  Each sub-tile of kSub
+// payloads is counting-sorted in LDS by local gene id, so every thread's kItems consecutive
+// payloads are long runs of one gene: registers accumulate a run; a run that ends inside the
+// thread's payloads goes to the LDS bins directly.  The run still open at the end of a sub-tile
+// stays in registers (in the next sub-tile the thread's positions mostly hold the same gene:
+// sub-tiles of one bucket have the same gene mix); lanes whose next payloads start another gene
+// flush together through the segmented DPP scan (gene_wave_flush), as do all open runs at the
+// end of the work item.
+template <bool k8>
+__device__ __forceinline__ void gene_reduce_item(const void* __restrict__ pay, int64_t beg, int64_t end, uint32_t g0,
+                                                 uint4* s_buf, int32_t* s_cbin, unsigned long long* s_lbin,
+                                                 uint32_t* s_cnt, uint32_t* s_start, uint64_t* s_scan,
+                                                 const double* s_rcp) {
+  using F = GeneFmt<k8>;
+  using W = typename F::W;
+  constexpr int kSub = F::kSub, kItems = kSub / kBlock;
+  static_assert(kSub * sizeof(W) == kGeneSub * sizeof(uint4), "one LDS buffer");
+  const W* src = reinterpret_cast<const W*>(pay);
+  W* s_sorted = reinterpret_cast<W*>(s_buf);
+  const int t = threadIdx.x;
+  GeneAcc acc;
+  acc.clear();
+  int cur = -1;
+  for (int64_t sub = beg; sub < end; sub += kSub) {
+    const int cnt = (int)((end - sub) < kSub ? (end - sub) : kSub);
+    if (t < kGenesPerBucket) s_cnt[t] = 0;
+    // rank on the gene word alone (clamped, unconditional loads: all in flight at once), then
+    // re-read the whole payload for the LDS scatter (an L2 hit)
+    uint32_t vx[kItems];  // local gene, then | rank << 8 (one register per item)
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      const int q = j * kBlock + t;
+      vx[j] = F::local(src + sub, q < cnt ? q : cnt - 1, g0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      const int q = j * kBlock + t;
+      const bool valid = q < cnt;
+      vx[j] |= block_rank(valid ? vx[j] : 0u, 6, valid, s_cnt) << 8;
+    }
+    __syncthreads();
+    {
+      uint64_t tot;
+      const uint32_t c = t < kGenesPerBucket ? s_cnt[t] : 0u;
+      const uint32_t st = (uint32_t)block_exclusive_scan<uint64_t>((uint64_t)c, &tot, s_scan);
+      if (t < kGenesPerBucket) s_start[t] = st;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      const int q = j * kBlock + t;
+      if (q < cnt) s_sorted[F::slot(s_start[vx[j] & 0xffu] + (vx[j] >> 8))] = src[sub + q];
+    }
+    __syncthreads();
+    // the thread's kItems consecutive sorted payloads; its open run continues if they start with
+    // its gene, else the wave's changed runs are flushed together first
+    const int j0 = t * kItems;
+    const int my_n = cnt - j0 < 0 ? 0 : (cnt - j0 < kItems ? cnt - j0 : kItems);
+    {
+      const int first = my_n > 0 ? (int)F::item(s_sorted[F::slot(j0)], g0).lg : cur;
+      const bool changed = cur >= 0 && first != cur;
+      if (__ballot(changed)) {
+        gene_wave_flush<k8>(acc, changed ? cur : -2 - (t & (kWave - 1)), s_cbin, s_lbin);
+        if (changed) {
+          acc.clear();
+          cur = -1;
+        }
+      }
+    }
+    for (int k = 0; k < my_n; k++) {
+      const GeneItem g = F::item(s_sorted[F::slot(j0 + k)], g0);
+      if ((int)g.lg != cur) {  // a gene boundary inside the thread's payloads: its own bin, no conflict
+        if (cur >= 0) acc.flush<k8>(&s_cbin[cur * kGeneCntPad], &s_lbin[cur * 3 * kStreamLanes]);
+        acc.clear();
+        cur = (int)g.lg;
+      }
+      acc.add(g, s_rcp);
+    }
+    __syncthreads();  // s_sorted / s_cnt are reused by the next sub-tile
+  }
+  // the threads' open runs, combined across each wave
+  gene_wave_flush<k8>(acc, cur, s_cbin, s_lbin);
+}
+
+// 3 waves per SIMD (the LDS allows 3 blocks per CU): <= 168 VGPRs, a few spills off the item loop
+// (measured 1.07 ms against 1.26 ms at the unconstrained 200 VGPRs, config 2)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) k_gene_reduce(const void* __restrict__ pay, const int64_t* __restrict__ work,
                                                         const int64_t* __restrict__ n_work, int32_t n_gene_ids,
+                                                        const uint32_t* __restrict__ gwide,
                                                         int64_t* __restrict__ partials) {
-  __shared__ uint4 s_sorted[kGeneSub];
+  __shared__ uint4 s_buf[kGeneSub];
   __shared__ int32_t s_cbin[kGenesPerBucket * kGeneCntPad];
   __shared__ unsigned long long s_lbin[kGenesPerBucket * 3 * kStreamLanes];
   __shared__ uint32_t s_cnt[kGenesPerBucket];
@@ -408,75 +561,10 @@ __global__ void __launch_bounds__(kBlock) k_gene_reduce(const GenePayload* __res
   const uint32_t g0 = (uint32_t)bucket * kGenesPerBucket;
   for (int i = t; i < kGenesPerBucket * kGeneCntPad; i += kBlock) s_cbin[i] = 0;
   for (int i = t; i < kGenesPerBucket * 3 * kStreamLanes; i += kBlock) s_lbin[i] = 0ull;
-  const uint4* src = reinterpret_cast<const uint4*>(pay);
-  GeneAcc acc;
-  acc.clear();
-  int cur = -1;
-  for (int64_t sub = beg; sub < end; sub += kGeneSub) {
-    const int cnt = (int)((end - sub) < kGeneSub ? (end - sub) : kGeneSub);
-    if (t < kGenesPerBucket) s_cnt[t] = 0;
-    // rank on the gene word alone (clamped, unconditional loads: all in flight at once), then
-    // re-read the whole payload for the LDS scatter (an L2 hit) -- 2 live VGPRs per item
-    const uint32_t* gw = reinterpret_cast<const uint32_t*>(src + sub);
-    uint32_t vx[kGeneItems], rk[kGeneItems];
-#pragma unroll
-    for (int j = 0; j < kGeneItems; j++) {
-      const int q = j * kBlock + t;
-      vx[j] = gw[4 * (q < cnt ? q : cnt - 1)];  // GenePayload.gene is the first word
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kGeneItems; j++) {
-      const int q = j * kBlock + t;
-      const bool valid = q < cnt;
-      rk[j] = block_rank(valid ? vx[j] - g0 : 0u, 6, valid, s_cnt);
-    }
-    __syncthreads();
-    {
-      uint64_t tot;
-      const uint32_t c = t < kGenesPerBucket ? s_cnt[t] : 0u;
-      const uint32_t st = (uint32_t)block_exclusive_scan<uint64_t>((uint64_t)c, &tot, s_scan);
-      if (t < kGenesPerBucket) s_start[t] = st;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kGeneItems; j++) {
-      const int q = j * kBlock + t;
-      if (q < cnt) s_sorted[gswz(s_start[vx[j] - g0] + rk[j])] = src[sub + q];
-    }
-    __syncthreads();
-    // the thread's kGeneItems consecutive sorted payloads; its open run continues if they start
-    // with its gene, else the wave's changed runs are flushed together first
-    const int j0 = t * kGeneItems;
-    const int my_n = cnt - j0 < 0 ? 0 : (cnt - j0 < kGeneItems ? cnt - j0 : kGeneItems);
-    {
-      const int first = my_n > 0 ? (int)(s_sorted[gswz(j0)].x - g0) : cur;
-      const bool changed = cur >= 0 && first != cur;
-      if (__ballot(changed)) {
-        gene_wave_flush(acc, changed ? cur : -2 - (t & (kWave - 1)), s_cbin, s_lbin);
-        if (changed) {
-          acc.clear();
-          cur = -1;
-        }
-      }
-    }
-    for (int k = 0; k < my_n; k++) {
-      const uint4 w = s_sorted[gswz(j0 + k)];
-      const GenePayload& g = *reinterpret_cast<const GenePayload*>(&w);
-      const int lg = (int)(g.gene - g0);
-      if (lg != cur) {  // a gene boundary inside the thread's payloads: its own bin, no conflict
-        if (cur >= 0) acc.flush(&s_cbin[cur * kGeneCntPad], &s_lbin[cur * 3 * kStreamLanes]);
-        acc.clear();
-        cur = lg;
-      }
-      acc.add(g, s_rcp);
-    }
-    // the thread's open run stays in registers: in a bucket's next sub-tile the thread's
-    // positions mostly hold the same gene again (sorted sub-tiles of the same gene mix)
-    __syncthreads();  // s_sorted / s_cnt are reused by the next sub-tile
-  }
-  // the threads' open runs, combined across each wave
-  gene_wave_flush(acc, cur, s_cbin, s_lbin);
+  if (*gwide)  // block-uniform
+    gene_reduce_item<false>(pay, beg, end, g0, s_buf, s_cbin, s_lbin, s_cnt, s_start, s_scan, s_rcp);
+  else
+    gene_reduce_item<true>(pay, beg, end, g0, s_buf, s_cbin, s_lbin, s_cnt, s_start, s_scan, s_rcp);
   __syncthreads();
   // bins -> partial rows: counter lanes 0..14 are partial slots 0..14; stream lanes follow P_FLOAT
   for (int i = t; i < kGenesPerBucket * kGeneCnt; i += kBlock) {

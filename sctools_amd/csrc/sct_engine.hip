@@ -289,17 +289,17 @@ template <bool kBucket, bool kStreams>
 int launch_build_keys(bool cell, bool gene, dim3 grid, hipStream_t s, const KeyCols& kc, const RecCols& rc2,
                       const uint8_t* mito, int64_t n, const uint64_t* toff, const Bits& b, uint64_t* keys,
                       void* vals, int64_t* ent_start, int64_t* partials, uint32_t* gcounts, int n_buckets,
-                      uint32_t* err) {
+                      uint32_t* err, uint32_t* gwide) {
   if (cell && gene) {
     LAUNCH_SHM("build_keys", (k_build_keys_run<true, true, kBucket, kStreams>), grid, dim3(kBlock),
                sizeof(uint32_t) * (size_t)n_buckets, s, kc, rc2, mito, n, toff, b, keys, vals, ent_start, partials,
-               gcounts, n_buckets, err);
+               gcounts, n_buckets, err, gwide);
   } else if (cell) {
     LAUNCH("build_keys", (k_build_keys_run<true, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito, n,
-           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err);
+           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide);
   } else {
     LAUNCH("build_keys", (k_build_keys_run<false, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito,
-           n, toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err);
+           n, toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide);
   }
   return SCT_OK;
 }
@@ -380,17 +380,21 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   const bool streams = exact && out_i;
   BucketCtl* ctl = bucket_ctl(ws, L);
   HIPCHK(hipMemsetAsync(ctl, 0, sizeof(BucketCtl), s));
+  // gene payload format: narrow (8 B) unless an operand does not fit (checked by the exact-stream
+  // pass; without it the wide format is used)
+  uint32_t* gwide = reinterpret_cast<uint32_t*>(at<uint64_t>(ws, L.scalars) + 16);
+  HIPCHK(hipMemsetAsync(gwide, streams ? 0 : 1, sizeof(uint32_t), s));
   if (bucket) {
     uint64_t* va = at<uint64_t>(ws, L.vals_a);
     rc = streams ? launch_build_keys<true, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
-                                                 partials, gcounts, L.n_buckets, &ctl->err)
+                                                 partials, gcounts, L.n_buckets, &ctl->err, gwide)
                  : launch_build_keys<true, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
-                                                  partials, gcounts, L.n_buckets, &ctl->err);
+                                                  partials, gcounts, L.n_buckets, &ctl->err, gwide);
   } else {
     rc = streams ? launch_build_keys<false, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
-                                                  ent_start, partials, gcounts, L.n_buckets, &ctl->err)
+                                                  ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide)
                  : launch_build_keys<false, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
-                                                   ent_start, partials, gcounts, L.n_buckets, &ctl->err);
+                                                   ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide);
     if (rc) return rc;
     uint32_t err = 0;  // the bucket path reads the flag at its first level sync
     if (int rb = readback(&err, &ctl->err, sizeof(err), s)) return rb;
@@ -457,15 +461,15 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     uint32_t* gcur = at<uint32_t>(ws, L.gcursor);
     int64_t* gwork = at<int64_t>(ws, L.gwork);
     int64_t* n_gwork = at<int64_t>(ws, L.scalars) + 4;
-    GenePayload* gpay = at<GenePayload>(ws, L.gpay);
+    void* gpay = at<GenePayload>(ws, L.gpay);
     LAUNCH_SHM("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), 2 * sizeof(uint32_t) * (size_t)(L.n_buckets + 1), s,
                (const uint32_t*)gcounts, L.n_buckets, gcur, gwork, n_gwork);
     LAUNCH_SHM("gene_emit", k_gene_emit, dim3((unsigned)cdiv(n, kEmitTile)), dim3(kBlock),
                2 * sizeof(uint32_t) * (size_t)L.n_buckets, s, rec->gene, rc2, (const uint16_t*)dflags, n, gcur,
-               L.n_buckets, gpay);
+               L.n_buckets, (const uint32_t*)gwide, gpay);
     HIPCHK(hipMemsetAsync(gene_partials, 0, sizeof(int64_t) * SCT_NP * (size_t)plan->n_gene_ids, s));
-    LAUNCH("gene_reduce", k_gene_reduce, dim3((unsigned)L.max_gene_work), dim3(kBlock), s, (const GenePayload*)gpay,
-           (const int64_t*)gwork, (const int64_t*)n_gwork, plan->n_gene_ids, gene_partials);
+    LAUNCH("gene_reduce", k_gene_reduce, dim3((unsigned)L.max_gene_work), dim3(kBlock), s, (const void*)gpay,
+           (const int64_t*)gwork, (const int64_t*)n_gwork, plan->n_gene_ids, (const uint32_t*)gwide, gene_partials);
   }
   if (n_rows) *n_rows = n_ent;
   return SCT_OK;

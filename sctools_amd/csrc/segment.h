@@ -189,9 +189,11 @@ __device__ __forceinline__ void tile_run_ids(const int32_t* __restrict__ ent, in
 // The exact fixed-point lanes of the quality streams for one tile whose run ids are in s_e
 // (tile_run_ids): blocked items (kItems consecutive records per thread) with 16-byte vector
 // loads; the streams are summed one after another so only 8 lanes are live per thread.
+// gwide (gene view): set when an operand exceeds the narrow gene payload (gene.h gene_payload8).
 template <bool kCell>
 __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int tile_n, const int32_t* s_e,
-                                            const double* s_rcp, int64_t* __restrict__ partials) {
+                                            const double* s_rcp, int64_t* __restrict__ partials,
+                                            uint32_t* __restrict__ gwide) {
   const int t = threadIdx.x;
   constexpr int ns = kCell ? 4 : 3;
   // numerator / denominator columns of half h of stream st: items q0 .. q0 + kItems - 1 of the thread's kKItems
@@ -241,6 +243,7 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
   // the next (stream, half)'s columns are loaded before the current one is summed (software
   // pipeline); a stream's lanes run over both halves and are flushed once
   uint32_t wn[8], wd[8], nn[8], nd[8];
+  uint32_t over = 0;  // operand bits above the narrow payload's fields (uy 5 bits, gq 9, gq_sum 15)
   load(0, 0, wn, wd);
 #pragma unroll 1
   for (int sh = 0; sh < 2 * ns; sh++) {
@@ -253,6 +256,8 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
       for (int i = 0; i < kStreamLanes; i++) lanes[i] = 0;
       cur_e = -1;
     }
+    const int osh = st == 0 ? 5 : st == 1 ? 9 : 15;
+    const uint32_t dmask = st < 2 ? ~0u : 0u, omask = st < 3 ? ~0u : 0u;
     const int slot0 = P_FLOAT + st * kStreamLanes;
     const auto slot = [slot0](int i) { return slot0 + i; };
 #pragma unroll
@@ -266,11 +271,13 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
       const uint32_t a = wide ? (wn[j / 2] >> (16 * (j % 2))) & 0xffffu : (wn[j / 4] >> (8 * (j % 4))) & 0xffu;
       const uint32_t d = wide ? (wd[j / 2] >> (16 * (j % 2))) & 0xffffu : (wd[j / 4] >> (8 * (j % 4))) & 0xffu;
       fx_accumulate(lanes, ratio_rcp(a, d, s_rcp));
+      over |= ((a | (d & dmask)) >> osh) & omask;
     }
     if (h == 1) wave_flush<kStreamLanes>(lanes, cur_e >= 0, cur_e, partials, slot);
 #pragma unroll
     for (int k = 0; k < 8; k++) wn[k] = nn[k], wd[k] = nd[k];
   }
+  if (gwide && __ballot(over != 0) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(gwide, 1u);
 }
 
 // kBucket: write the bucket path's 16-byte payload (bucket.h: w0 = key' | ref | strand |
@@ -288,7 +295,7 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
                                                            int64_t* __restrict__ ent_start,
                                                            int64_t* __restrict__ partials,
                                                            uint32_t* __restrict__ gene_counts, int n_buckets,
-                                                           uint32_t* __restrict__ err) {
+                                                           uint32_t* __restrict__ err, uint32_t* __restrict__ gwide) {
   static_assert(!kGene || kCell, "gene buckets come from the cell view");
   __shared__ int32_t s_e[kTilePad];
   __shared__ int32_t s_prev;
@@ -388,7 +395,7 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
     for (int i = t; i < n_buckets; i += kBlock)
       if (s_hist[i]) atomicAdd(&gene_counts[i], s_hist[i]);
   }
-  if constexpr (kStreams) stream_tile<kCell>(r, base, tile_n, s_e, s_rcp, partials);
+  if constexpr (kStreams) stream_tile<kCell>(r, base, tile_n, s_e, s_rcp, partials, kGene ? gwide : nullptr);
 }
 
 }  // namespace sct

@@ -192,6 +192,44 @@ def test_combined_cell_and_gene_pass(eng):
     compare(gi[live], gf[live], oi[live], of[live], exact_floats=False)
 
 
+@pytest.mark.parametrize("case", ["at_limits", "over_limits"])
+def test_gene_payload_formats(eng, case):
+    """Grouped gene partials use the 8-byte payload when every stream operand fits its field
+    (uy <= 31, gq <= 511, gq_sum <= 32767: gene.h gene_payload8) and the 16-byte one otherwise;
+    the rows equal the oracle's either way, and the one-pass partials equal the gene-only pass's
+    (which always uses the 16-byte payload)."""
+    from sctools_amd import engine as E
+
+    d = gpu_synth(400_000, 80, 4_000, 26)
+    cols = {c: t.clone() for c, t in d.cols.items()}
+    n = cols["cell"].numel()
+    gen = torch.Generator().manual_seed(9)
+    idx = torch.randperm(n, generator=gen)[: n // 40].to(eng.device)
+    k = idx.numel()
+    uy, gq, gs = (31, 511, 32767) if case == "at_limits" else (40, 600, 40000)
+    rnd = torch.rand(k, generator=gen).to(eng.device)
+    cols["uy_len"][idx] = uy
+    cols["uy_gt30"][idx] = (rnd * (uy + 1)).to(torch.uint8).clamp(max=uy)
+    cols["gq_len"][idx] = gq
+    cols["gq_gt30"][idx] = (rnd * (gq + 1)).to(torch.int32).clamp(max=gq).to(torch.int16)
+    cols["gq_sum"][idx] = torch.tensor(gs, dtype=torch.int32).to(torch.int16).item()  # uint16 bits
+    dims = E.Dims(d.n_cell_ids, d.n_gene_ids, d.n_umi_ids)
+    mito = torch.from_numpy(d.gene_is_mito).to(eng.device)
+    ci, cf, part = eng.cell_and_gene(cols, dims, mito)
+    assert torch.equal(part, eng.gene_partials(cols, dims))
+    h = {c: t.cpu().numpy() for c, t in cols.items()}
+    for c in ("gq_sum", "gq_len", "gq_gt30"):
+        h[c] = h[c].view(np.uint16)
+    assert int(h["gq_sum"].max()) == gs and int(h["uy_len"].max()) == uy
+    oi, of = O.run(h, "gene_grouped", d.gene_is_mito, d.n_gene_ids, threads=8)
+    gi, gf = eng.finalize_partials(part)
+    gi, gf = gi.cpu().numpy(), gf.cpu().numpy()
+    live = oi[:, 0] > 0
+    compare(gi[live], gf[live], oi[live], of[live], exact_floats=False)
+    oi, of = O.run(h, "cell", d.gene_is_mito, d.n_gene_ids, threads=8)
+    compare(ci.cpu().numpy(), cf.cpu().numpy(), oi, of, exact_floats=False)
+
+
 def test_grouped_needs_cell_sorted_input(eng):
     from sctools_amd import _native as N
 
