@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="time the steps without per-kernel HIP events (no roofline / kernel table)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the record-count sanity checks (timing experimental engine builds only)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5],
                     help="2: cell-sorted records (default); 4: the 1B-read atlas per GPU of 8 -- 125M records, 62.5k "
                          "cells with lognormal(0, 2) reads; 5: globally shuffled records, 30%% NH>1, 40%% duplicates, "
@@ -217,8 +219,9 @@ def main():
 
     # sanity: every record accounted on both sides
     n_cell_reads = int(host_cells[:rows, 0].sum())
-    assert n_cell_reads == args.records, (n_cell_reads, args.records)
-    assert int(host_genei[:, 0].sum()) == args.records * world
+    if not args.no_check:
+        assert n_cell_reads == args.records, (n_cell_reads, args.records)
+        assert int(host_genei[:, 0].sum()) == args.records * world
 
     total_records = args.records * world * args.steps
     value = total_records / elapsed
