@@ -256,8 +256,13 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
       for (int i = 0; i < kStreamLanes; i++) lanes[i] = 0;
       cur_e = -1;
     }
-    const int osh = st == 0 ? 5 : st == 1 ? 9 : 15;
-    const uint32_t dmask = st < 2 ? ~0u : 0u, omask = st < 3 ? ~0u : 0u;
+    {  // on the packed columns: uy (u8) above 31, gq_gt30 / gq_len (u16) above 511, gq_sum above 32767
+      const uint32_t m = st == 0 ? 0xE0E0E0E0u : st == 1 ? 0xFE00FE00u : st == 2 ? 0x80008000u : 0u;
+      uint32_t o = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) o |= wn[k] | (st < 2 ? wd[k] : 0u);
+      over |= o & m;
+    }
     const int slot0 = P_FLOAT + st * kStreamLanes;
     const auto slot = [slot0](int i) { return slot0 + i; };
 #pragma unroll
@@ -271,7 +276,6 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
       const uint32_t a = wide ? (wn[j / 2] >> (16 * (j % 2))) & 0xffffu : (wn[j / 4] >> (8 * (j % 4))) & 0xffu;
       const uint32_t d = wide ? (wd[j / 2] >> (16 * (j % 2))) & 0xffffu : (wd[j / 4] >> (8 * (j % 4))) & 0xffu;
       fx_accumulate(lanes, ratio_rcp(a, d, s_rcp));
-      over |= ((a | (d & dmask)) >> osh) & omask;
     }
     if (h == 1) wave_flush<kStreamLanes>(lanes, cur_e >= 0, cur_e, partials, slot);
 #pragma unroll
