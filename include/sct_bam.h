@@ -38,9 +38,15 @@ extern "C" {
                                 * molecule / gene tags, XF and the query name are read, nothing is
                                 * validated, an empty file is 0 records, and the "qhead" column is set */
 
+#define SCT_BAM_SORT_KEYS 3   /* TagSortBam / VerifyBamSort keys (bam.py:638-724): the three dictionary tags
+                                * (a missing tag and an empty value are both id 0: get_tag_or_default's "")
+                                * and the query name, ranked into a fourth dictionary (column "qname",
+                                * int32); nothing is validated, an empty file is 0 records */
+
 #define SCT_BAM_TAG_CB 0
 #define SCT_BAM_TAG_UB 1
 #define SCT_BAM_TAG_GE 2
+#define SCT_BAM_QNAME 3 /* SCT_BAM_SORT_KEYS: the query-name dictionary */
 
 typedef struct sct_bam sct_bam_t;
 
@@ -65,11 +71,12 @@ int64_t sct_bam_n(const sct_bam_t* b);
 /* Host pointer to a column by name (the sct_records_t field names: "cell", "umi", "gene",
  * "ref", "pos", "gq_sum", "gq_len", "gq_gt30", "bits", "xf", "cy_gt30", "cy_len",
  * "uy_gt30", "uy_len"), or "qhead" (uint8: 1 where the record's query name differs from the
- * previous record's -- the itertools.groupby of count.py:83-86 -- SCT_BAM_COUNT_MATRIX only);
+ * previous record's -- the itertools.groupby of count.py:83-86 -- SCT_BAM_COUNT_MATRIX only),
+ * or "qname" (int32 rank of the query name, SCT_BAM_SORT_KEYS only);
  * NULL for an unknown name.  Valid until sct_bam_close. */
 const void* sct_bam_column(const sct_bam_t* b, const char* name);
 
-/* Dictionary of tag `which` (SCT_BAM_TAG_*): *n entries in id order; entry i is the UTF-8
+/* Dictionary of tag `which` (SCT_BAM_TAG_*, or SCT_BAM_QNAME): *n entries in id order; entry i is the UTF-8
  * string bytes[offsets[i] .. offsets[i + 1]); *has_none = 1 when id 0 is the missing value
  * (its bytes are empty). */
 int sct_bam_dictionary(const sct_bam_t* b, int32_t which, int64_t* n, const char** bytes,
@@ -91,6 +98,13 @@ void sct_bam_close(sct_bam_t* b);
 int sct_bam_split(const char* const* in_paths, int32_t n_in, const char* out_prefix, const char* tags,
                   int32_t n_tags, int32_t n_subfiles, int32_t raise_missing, int32_t level, int32_t n_threads,
                   int32_t* n_out, int64_t* bad_record);
+
+/* TagSortBam's output (platform.py:60-97, pysam writes the sorted records under the input's
+ * header): the records of `in_path` written to `out_path` in the order `perm` gives
+ * (perm[k] = the input index of output record k, a permutation of 0..n-1), byte for byte,
+ * as BGZF (header members, 0xff00-byte record members, EOF) at zlib `level`. */
+int sct_bam_write_order(const char* in_path, const char* out_path, const int64_t* perm, int64_t n, int32_t level,
+                        int32_t n_threads);
 
 #ifdef __cplusplus
 }

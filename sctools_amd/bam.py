@@ -22,7 +22,10 @@ native one against; BAM input of the metric path goes through the native
 multi-threaded decoder (``sctools_amd/csrc/bamdec.cpp``).
 
 ``split`` is SplitBam (``bam.py:361-488``) on the native splitter
-(``sctools_amd/csrc/bamsplit.cpp``).
+(``sctools_amd/csrc/bamsplit.cpp``).  ``TagSortableRecord`` / ``verify_sort`` /
+``sort_by_tags_and_queryname`` mirror the reference's sort order on record objects
+(``bam.py:602-728``); ``verify_bam_sort`` checks a whole BAM on the GPU (VerifyBamSort) and
+``tag_sort_bam`` writes one in that order (TagSortBam).
 """
 
 import math
@@ -36,7 +39,8 @@ from typing import Dict, Iterator, List, Optional, Set, Tuple
 from sctools_amd import consts
 
 __all__ = ["BamRecord", "open_alignments", "read_header", "split", "get_barcodes_from_bam",
-           "get_barcode_for_alignment"]
+           "get_barcode_for_alignment", "SortError", "TagSortableRecord", "get_tag_or_default",
+           "sort_by_tags_and_queryname", "verify_sort", "verify_bam_sort", "tag_sort_bam"]
 
 _CIGAR_OPS = "MIDNSHP=X"
 _SEQ_NT16 = "=ACMGRSVTWYHKDBN"
@@ -393,3 +397,193 @@ def split(in_bams: List[str], out_prefix: str, tags: List[str], approx_mb_per_sp
     n = bamnative.split(list(in_bams), out_prefix, list(tags), max(1, n_subfiles), raise_missing,
                         threads=num_processes)
     return [os.path.realpath("%s_%d.bam" % (out_prefix, k)) for k in range(n)]
+
+
+# ---------------- TagSortBam / VerifyBamSort order (bam.py:602-728) ----------------
+class SortError(Exception):
+    """Records out of (tags, query name) order (bam.py:727-728)."""
+
+
+def get_tag_or_default(alignment, tag_key: str, default: Optional[str] = None):
+    """The tag's value, or ``default`` when the alignment lacks it (bam.py:602-610)."""
+    try:
+        return alignment.get_tag(tag_key)
+    except KeyError:
+        return default
+
+
+class TagSortableRecord:
+    """A record keyed by its tag values, then its query name (bam.py:638-695): the order of
+    ``sort_by_tags_and_queryname`` and ``verify_sort``; comparing records keyed by different tag
+    lists raises ValueError."""
+
+    def __init__(self, tag_keys, tag_values, query_name: str, record=None) -> None:
+        self.tag_keys = tag_keys
+        self.tag_values = tag_values
+        self.query_name = query_name
+        self.record = record
+
+    @classmethod
+    def from_aligned_segment(cls, record, tag_keys) -> "TagSortableRecord":
+        assert record is not None
+        return cls(tag_keys, [get_tag_or_default(record, key, "") for key in tag_keys], record.query_name, record)
+
+    def _check(self, other) -> None:
+        if self.tag_keys != other.tag_keys:
+            raise ValueError("Cannot compare records using different tag lists: {0}, {1}".format(
+                self.tag_keys, other.tag_keys))
+
+    def _key(self):
+        return (list(self.tag_values), self.query_name)
+
+    def __lt__(self, other) -> bool:
+        if not isinstance(other, TagSortableRecord):
+            return NotImplemented
+        self._check(other)
+        return self._key() < other._key()
+
+    def __eq__(self, other) -> bool:
+        if not isinstance(other, TagSortableRecord):
+            return NotImplemented
+        self._check(other)
+        return self._key() == other._key()
+
+    def __le__(self, other) -> bool:
+        return self < other or self == other
+
+    def __gt__(self, other) -> bool:
+        if not isinstance(other, TagSortableRecord):
+            return NotImplemented
+        return other < self
+
+    def __ge__(self, other) -> bool:
+        if not isinstance(other, TagSortableRecord):
+            return NotImplemented
+        return other < self or self == other
+
+    __hash__ = None
+
+    def __repr__(self) -> str:
+        return "TagSortableRecord(tags: {0}, tag_values: {1}, query_name: {2}".format(
+            self.tag_keys, self.tag_values, self.query_name)
+
+    __str__ = __repr__
+
+
+def sort_by_tags_and_queryname(records, tag_keys):
+    """The records in (tag values, query name) order, stable (bam.py:698-709)."""
+    return (r.record for r in sorted(TagSortableRecord.from_aligned_segment(r, tag_keys) for r in records))
+
+
+def _order_error(i: int, record, old_record) -> SortError:
+    msg = "Records {0} and {1} are not in correct order:\n{1}:{2} \nis less than \n{0}:{3}"
+    return SortError(msg.format(i - 1, i, record, old_record))
+
+
+def verify_sort(records, tag_keys) -> None:
+    """Raise SortError at the first record smaller than its predecessor (bam.py:712-724)."""
+    old = TagSortableRecord(tag_keys=tag_keys, tag_values=["" for _ in tag_keys], query_name="", record=None)
+    i = 0
+    for record in records:
+        i += 1
+        if not record >= old:
+            raise _order_error(i, record, old)
+        old = record
+
+
+def _sort_keys(path: str, tag_keys):
+    """(keys, key names, query-name ranks, query names) of a BAM: up to three tags as ranks of
+    their sorted string values (native decode, "" for a missing tag), more as ranks of the
+    value tuples (host); query names as ranks of the sorted names."""
+    import numpy as np
+
+    from sctools_amd import bamnative
+
+    if len(tag_keys) <= 3:
+        pad = [t for t in ("~0", "~1", "~2") if t not in tag_keys][: 3 - len(tag_keys)]
+        arrays, names = bamnative.decode(path, "sortkeys", tags=tuple(list(tag_keys) + pad))
+        keys = [arrays["cell"], arrays["umi"], arrays["gene"]][: len(tag_keys)]
+        key_names = [["" if v is None else v for v in nm] for nm in names[: len(tag_keys)]]
+        return keys, key_names, arrays["qname"], names[3]
+    # more tags than the native key columns (rare: the reference CLIs pass three): tuples on the host
+    recs = [(tuple("" if v is None else str(v) for v in (get_tag_or_default(r, k, "") for k in tag_keys)),
+             r.query_name) for r in open_alignments(path, "rb")]
+    tuples = sorted(set(t for t, _ in recs))
+    trank = {t: i for i, t in enumerate(tuples)}
+    qs = sorted(set(q for _, q in recs))
+    qr = {q: i for i, q in enumerate(qs)}
+    return ([np.array([trank[t] for t, _ in recs], dtype=np.int32)], [[list(t) for t in tuples]],
+            np.array([qr[q] for _, q in recs], dtype=np.int32), qs)
+
+
+def _key_columns(eng, keys, key_names, n):
+    """Record columns carrying the sort keys (cell, umi, gene slots), Dims and the order name."""
+    import numpy as np
+    import torch
+
+    from sctools_amd import engine as E
+    from sctools_amd import _native as N
+
+    cols = {c: torch.zeros(n, dtype=E._TORCH_DTYPES[c], device=eng.device) for c in N.RECORD_COLUMNS}
+    for slot, k in zip(("cell", "umi", "gene"), keys):
+        cols[slot] = torch.from_numpy(np.ascontiguousarray(k, dtype=np.int32)).to(eng.device)
+    size = [max(1, len(nm)) for nm in key_names] + [1] * (3 - len(key_names))
+    dims = E.Dims(size[0], size[2], size[1])  # (cell, gene, umi) id counts
+    return cols, dims, ("cell" if len(keys) <= 1 else "cell_umi_gene")
+
+
+def verify_bam_sort(path: str, tag_keys, device=None) -> None:
+    """VerifyBamSort on a BAM file (platform.py:100-143): the records decoded natively (the
+    tags' values and the query names as ranks of their sorted strings, bamdec.cpp sort-key
+    mode) and checked on the GPU (sct_verify_sort); raises SortError as verify_sort does."""
+    import numpy as np
+    import torch
+
+    from sctools_amd import engine as E
+
+    tag_keys = list(tag_keys)
+    keys, key_names, qrank, qnames = _sort_keys(path, tag_keys)
+    n = int(qrank.shape[0])
+    if n < 2:
+        return
+    eng = E.get_engine(device)
+    cols, dims, order = _key_columns(eng, keys, key_names, n)
+    tie = torch.from_numpy(np.ascontiguousarray(qrank, dtype=np.int32)).to(eng.device)
+    p = eng.verify_sort(cols, dims, order, tie)
+    if p < 0:
+        return
+
+    def record(j):
+        if len(tag_keys) <= 3:
+            vals = [key_names[k][int(keys[k][j])] for k in range(len(tag_keys))]
+        else:
+            vals = list(key_names[0][int(keys[0][j])])
+        return TagSortableRecord(tag_keys, vals, qnames[int(qrank[j])])
+
+    raise _order_error(p + 1, record(p), record(p - 1))
+
+
+def tag_sort_bam(in_bam: str, out_bam: str, tag_keys, device=None, level: int = 6) -> None:
+    """TagSortBam (platform.py:60-97): the records of ``in_bam`` written to ``out_bam`` in
+    (tags, query name) order, ties in input order (sort_by_tags_and_queryname's stable
+    sorted()): keys decoded natively, the order computed on the GPU (sct_tag_sort: one radix
+    round on the packed tag ranks, the query-name rank as the tiebreak), the records written
+    byte for byte under the input's header (sct_bam_write_order)."""
+    import numpy as np
+    import torch
+
+    from sctools_amd import bamnative
+    from sctools_amd import engine as E
+
+    tag_keys = list(tag_keys)
+    keys, key_names, qrank, qnames = _sort_keys(in_bam, tag_keys)
+    n = int(qrank.shape[0])
+    if n == 0:
+        bamnative.write_order(in_bam, out_bam, np.zeros(0, np.int64), level=level)
+        return
+    eng = E.get_engine(device)
+    cols, dims, order = _key_columns(eng, keys, key_names, n)
+    cols["pos"] = torch.arange(n, dtype=torch.int32, device=eng.device)  # rides along: the permutation
+    tie = torch.from_numpy(np.ascontiguousarray(qrank, dtype=np.int32)).to(eng.device)
+    out = eng.tag_sort(cols, dims, order, tie, len(qnames))
+    bamnative.write_order(in_bam, out_bam, out["pos"].to(torch.int64).cpu().numpy(), level=level)

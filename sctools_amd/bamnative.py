@@ -20,10 +20,10 @@ LIB_PATH = os.path.join(HERE, "libsct_bam.so")
 
 OK, EIO, EFORMAT = 0, -1, -2
 KEYERROR, TYPEERROR, ZERODIV, VALUEERROR, EMPTY, MISSING_TAG = -10, -11, -12, -13, -14, -15
-CELL_METRICS, GENE_METRICS, COUNT_MATRIX = 0, 1, 2
-_MODES = {"cell": CELL_METRICS, "gene": GENE_METRICS, "count": COUNT_MATRIX}
+CELL_METRICS, GENE_METRICS, COUNT_MATRIX, SORT_KEYS = 0, 1, 2, 3
+_MODES = {"cell": CELL_METRICS, "gene": GENE_METRICS, "count": COUNT_MATRIX, "sortkeys": SORT_KEYS}
 EXPORTED = ("sct_bam_decode", "sct_bam_decode_tags", "sct_bam_last_error", "sct_bam_n", "sct_bam_column", "sct_bam_dictionary",
-            "sct_bam_close", "sct_bam_split")
+            "sct_bam_close", "sct_bam_split", "sct_bam_write_order")
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -57,6 +57,8 @@ def load() -> ctypes.CDLL:
     L.sct_bam_split.restype = ctypes.c_int
     L.sct_bam_split.argtypes = [ctypes.POINTER(ctypes.c_char_p), i32, ctypes.c_char_p, ctypes.c_char_p, i32, i32, i32,
                                 i32, i32, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_int64)]
+    L.sct_bam_write_order.restype = ctypes.c_int
+    L.sct_bam_write_order.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, ctypes.c_int64, i32, i32]
     _lib = L
     return L
 
@@ -74,7 +76,12 @@ def decode(path: str, metric_mode: str = "cell", threads: int = 0, tags=("CB", "
 
     metric_mode "count" (CountMatrix): only cell / umi / gene / xf are meaningful, the three
     dictionary tags are ``tags``, nothing is validated, and ``arrays["qhead"]`` marks the first
-    record of each run of equal query names."""
+    record of each run of equal query names.
+
+    metric_mode "sortkeys" (TagSortBam / VerifyBamSort): cell / umi / gene are the ranks of the
+    three ``tags`` (a missing tag and an empty value both rank first, as "" does),
+    ``arrays["qname"]`` the rank of the query name, and a fourth name list holds the query
+    names in rank order."""
     from sctools_amd.columnar import COLUMNS
 
     L = load()
@@ -91,13 +98,14 @@ def decode(path: str, metric_mode: str = "cell", threads: int = 0, tags=("CB", "
     try:
         n = int(L.sct_bam_n(h))
         arrays = {}
-        cols = list(COLUMNS) + ([("qhead", np.uint8)] if metric_mode == "count" else [])
+        extra = {"count": [("qhead", np.uint8)], "sortkeys": [("qname", np.int32)]}
+        cols = list(COLUMNS) + extra.get(metric_mode, [])
         for name, dt in cols:
             ptr = L.sct_bam_column(h, name.encode())
             buf = (ctypes.c_char * (n * np.dtype(dt).itemsize)).from_address(ptr) if n else b""
             arrays[name] = np.frombuffer(buf, dtype=dt, count=n).copy()
         names = []
-        for which in range(3):
+        for which in range(4 if metric_mode == "sortkeys" else 3):
             cnt, by, off, hn = ctypes.c_int64(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int32()
             L.sct_bam_dictionary(h, which, ctypes.byref(cnt), ctypes.byref(by), ctypes.byref(off), ctypes.byref(hn))
             k = int(cnt.value)
@@ -129,3 +137,14 @@ def split(in_paths, out_prefix: str, tags, n_subfiles: int, raise_missing: bool 
     if rc != OK:
         raise _EXC.get(rc, RuntimeError)(L.sct_bam_last_error().decode("utf-8", "replace"))
     return int(n_out.value)
+
+
+def write_order(in_path: str, out_path: str, perm, level: int = 6, threads: int = 0) -> None:
+    """sct_bam_write_order: the records of ``in_path`` in the order ``perm`` (output record k is
+    input record perm[k]) under the input's header."""
+    L = load()
+    p = np.ascontiguousarray(perm, dtype=np.int64)
+    rc = L.sct_bam_write_order(os.fsencode(in_path), os.fsencode(out_path), p.ctypes.data if p.size else None,
+                               int(p.size), int(level), int(threads))
+    if rc != OK:
+        raise _EXC.get(rc, RuntimeError)(L.sct_bam_last_error().decode("utf-8", "replace"))

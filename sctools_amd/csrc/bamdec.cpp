@@ -57,7 +57,8 @@ struct Columns {
   std::vector<int32_t> cell, umi, gene, ref, pos;
   std::vector<uint16_t> gq_sum, gq_len, gq_gt30;
   std::vector<uint8_t> bits, xf, cy_gt30, cy_len, uy_gt30, uy_len;
-  std::vector<uint8_t> qhead;  // count-matrix mode only
+  std::vector<uint8_t> qhead;   // count-matrix mode only
+  std::vector<int32_t> qname;   // sort-key mode only
   void resize(size_t n) {
     cell.resize(n), umi.resize(n), gene.resize(n), ref.resize(n), pos.resize(n);
     gq_sum.resize(n), gq_len.resize(n), gq_gt30.resize(n);
@@ -390,9 +391,9 @@ int32_t intern_tag(Interner& in, TagCache& c, TagVal& v, std::string& tmp) {
 struct sct_bam {
   Columns c;
   int64_t n = 0;
-  std::string dict_bytes[3];
-  std::vector<int64_t> dict_off[3];
-  int32_t has_none[3] = {0, 0, 0};
+  std::string dict_bytes[4];  // CB, UB, GE (or the three named tags), query names (sort-key mode)
+  std::vector<int64_t> dict_off[4];
+  int32_t has_none[4] = {0, 0, 0, 0};
 };
 
 extern "C" {
@@ -409,11 +410,13 @@ int sct_bam_decode_tags(const char* path, int32_t metric_mode, const char* tags,
   if (out) *out = nullptr;
   if (bad_record) *bad_record = -1;
   if (!path || !out || !tags) return fail(SCT_BAM_EIO, "NULL argument");
-  if (metric_mode < SCT_BAM_CELL_METRICS || metric_mode > SCT_BAM_COUNT_MATRIX)
+  if (metric_mode < SCT_BAM_CELL_METRICS || metric_mode > SCT_BAM_SORT_KEYS)
     return fail(SCT_BAM_EIO, "unknown decode mode %d", metric_mode);
   if (strlen(tags) != 6) return fail(SCT_BAM_EIO, "tags must name three two-character tags");
+  const bool sortkeys = metric_mode == SCT_BAM_SORT_KEYS;
   const bool counting = metric_mode == SCT_BAM_COUNT_MATRIX;
-  if (!counting && memcmp(tags, "CBUBGE", 6) != 0) return fail(SCT_BAM_EIO, "the metric modes read CB / UB / GE");
+  const bool generic = counting || sortkeys;  // named tags, no validation
+  if (!generic && memcmp(tags, "CBUBGE", 6) != 0) return fail(SCT_BAM_EIO, "the metric modes read CB / UB / GE");
   const bool is_cell = metric_mode == SCT_BAM_CELL_METRICS;
   if (n_threads <= 0) n_threads = omp_get_max_threads();
   const int fd = open(path, O_RDONLY);
@@ -444,8 +447,8 @@ int sct_bam_decode_tags(const char* path, int32_t metric_mode, const char* tags,
 
   sct_bam* B = new sct_bam();
   std::unique_ptr<sct_bam> guard(B);
-  Interner dicts[3];
-  std::atomic<int32_t> has_none[3];
+  Interner dicts[4];
+  std::atomic<int32_t> has_none[4];
   for (auto& h : has_none) h = 0;
 
   // carry + this window's inflated bytes; grown without zero-filling (inflate writes every byte)
@@ -534,6 +537,7 @@ int sct_bam_decode_tags(const char* path, int32_t metric_mode, const char* tags,
     const int64_t nw = (int64_t)starts.size();
     B->c.resize((size_t)(base + nw));
     if (counting) B->c.qhead.resize((size_t)(base + nw));
+    if (sortkeys) B->c.qname.resize((size_t)(base + nw));
     std::atomic<int64_t> first_bad{INT64_MAX};
     std::mutex err_m;
     RecErr first_err;
@@ -543,14 +547,14 @@ int sct_bam_decode_tags(const char* path, int32_t metric_mode, const char* tags,
       std::string tmp;
       Parsed o;
       RecErr e;
-      std::unique_ptr<TagCache[]> cache(new TagCache[3]);
+      std::unique_ptr<TagCache[]> cache(new TagCache[4]);
 #pragma omp for schedule(dynamic, 4096)
       for (int64_t i = 0; i < nw; i++) {
         const uint8_t* d = buf.data() + starts[i] + 4;
         const uint32_t bs = rd32(buf.data() + starts[i]);
         const char* qn = nullptr;
         uint32_t qlen = 0;
-        if (counting ? parse_count_record(d, bs, tags, o, &qn, &qlen, e) : parse_record(d, bs, is_cell, o, e)) {
+        if (generic ? parse_count_record(d, bs, tags, o, &qn, &qlen, e) : parse_record(d, bs, is_cell, o, e)) {
           std::lock_guard<std::mutex> lk(err_m);
           if (base + i < first_bad.load()) {
             first_bad = base + i;
@@ -572,6 +576,13 @@ int sct_bam_decode_tags(const char* path, int32_t metric_mode, const char* tags,
         C.bits[j] = o.bits, C.xf[j] = o.xf;
         C.cy_gt30[j] = (uint8_t)o.cy_gt30, C.cy_len[j] = (uint8_t)o.cy_len;
         C.uy_gt30[j] = (uint8_t)o.uy_gt30, C.uy_len[j] = (uint8_t)o.uy_len;
+        if (sortkeys) {  // get_tag_or_default(record, key, ""): an empty value sorts as a missing one
+          C.qname[j] = intern_bytes(dicts[3], cache[3], qn, qlen);
+          for (TagVal* v : {&o.cb, &o.ub, &o.ge}) {
+            as_str(*v);
+            if (v->present && v->n == 0) v->present = false;
+          }
+        }
         C.cell[j] = intern_tag(dicts[0], cache[0], o.cb, tmp);
         C.umi[j] = intern_tag(dicts[1], cache[1], o.ub, tmp);
         C.gene[j] = intern_tag(dicts[2], cache[2], o.ge, tmp);
@@ -598,9 +609,9 @@ int sct_bam_decode_tags(const char* path, int32_t metric_mode, const char* tags,
     if (bi == blocks.size() && carry == 0) break;
   }
   B->n = base;
-  if (base == 0 && !counting) return fail(SCT_BAM_EMPTY, "generator raised StopIteration");
+  if (base == 0 && !generic) return fail(SCT_BAM_EMPTY, "generator raised StopIteration");
   // 5. rank the dictionaries: sorted strings, the missing value first
-  for (int t = 0; t < 3; t++) {
+  for (int t = 0; t < (sortkeys ? 4 : 3); t++) {
     std::vector<std::pair<std::string, int32_t>> all;
     dicts[t].collect(all);
     std::sort(all.begin(), all.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
@@ -614,7 +625,7 @@ int sct_bam_decode_tags(const char* path, int32_t metric_mode, const char* tags,
       B->dict_bytes[t] += all[r].first;
       B->dict_off[t].push_back((int64_t)B->dict_bytes[t].size());
     }
-    std::vector<int32_t>& col = t == 0 ? B->c.cell : t == 1 ? B->c.umi : B->c.gene;
+    std::vector<int32_t>& col = t == 0 ? B->c.cell : t == 1 ? B->c.umi : t == 2 ? B->c.gene : B->c.qname;
 #pragma omp parallel for num_threads(n_threads) schedule(static)
     for (int64_t i = 0; i < base; i++) col[i] = rank[col[i]];
   }
@@ -646,14 +657,15 @@ const void* sct_bam_column(const sct_bam_t* b, const char* name) {
   if (s == "uy_gt30") return c.uy_gt30.data();
   if (s == "uy_len") return c.uy_len.data();
   if (s == "qhead") return c.qhead.empty() && b->n ? nullptr : c.qhead.data();
+  if (s == "qname") return c.qname.empty() && b->n ? nullptr : c.qname.data();
   return nullptr;
 }
 
 int sct_bam_dictionary(const sct_bam_t* b, int32_t which, int64_t* n, const char** bytes, const int64_t** offsets,
                        int32_t* has_none) {
-  if (!b || which < 0 || which > 2 || !n || !bytes || !offsets || !has_none)
+  if (!b || which < 0 || which > 3 || !n || !bytes || !offsets || !has_none)
     return fail(SCT_BAM_EIO, "bad sct_bam_dictionary arguments");
-  *n = (int64_t)b->dict_off[which].size() - 1;
+  *n = b->dict_off[which].empty() ? 0 : (int64_t)b->dict_off[which].size() - 1;
   *bytes = b->dict_bytes[which].data();
   *offsets = b->dict_off[which].data();
   *has_none = b->has_none[which];

@@ -412,4 +412,110 @@ int sct_bam_split(const char* const* in_paths, int32_t n_in, const char* out_pre
   return SCT_BAM_OK;
 }
 
+// TagSortBam's output (platform.py:60-97): the input's records in the order `perm` gives
+// (perm[k] = input index of output record k), byte for byte, under the input's header.  The
+// inflated records are held in memory (the reference holds every record in Python too); the
+// output stream is assembled with parallel copies and deflated in parallel 0xff00-byte pieces.
+int sct_bam_write_order(const char* in_path, const char* out_path, const int64_t* perm, int64_t n, int32_t level,
+                        int32_t n_threads) {
+  g_err.clear();
+  if (!in_path || !out_path || n < 0 || (n > 0 && !perm)) return fail(SCT_BAM_EIO, "bad arguments");
+  if (level < 0 || level > 9) return fail(SCT_BAM_EIO, "compression level %d outside 0..9", level);
+  if (n_threads <= 0) n_threads = omp_get_max_threads();
+  Mapped m;
+  int rc = map_bam(in_path, m);
+  if (rc) return rc;
+  Walker w(m, n_threads);
+  std::vector<uint8_t> recs;   // every record (block_size field included), in file order
+  std::vector<uint64_t> at;    // record start in recs
+  std::string header0;
+  while ((rc = w.next(in_path)) == 1) {
+    if (at.empty() && header0.empty()) header0 = w.header;
+    if (!w.starts.empty()) {
+      const uint64_t first = w.starts.front();
+      const uint64_t last = w.starts.back() + 4 + rd32(w.buf.data() + w.starts.back());
+      const uint64_t base = recs.size();
+      recs.insert(recs.end(), w.buf.begin() + first, w.buf.begin() + last);
+      for (uint64_t o : w.starts) at.push_back(base + (o - first));
+    }
+    w.advance();
+  }
+  if (rc < 0) return rc;
+  if (header0.empty()) header0 = w.header;
+  if ((int64_t)at.size() != n) return fail(SCT_BAM_EIO, "%s holds %zu records, the order %lld", in_path, at.size(), (long long)n);
+  // output offsets: the permuted records' sizes, scanned per thread
+  const int T = n_threads;
+  std::vector<uint64_t> part(T + 1, 0);
+  int bad = 0;
+#pragma omp parallel num_threads(T) reduction(| : bad)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+    uint64_t sz = 0;
+    for (int64_t k = lo; k < hi; k++) {
+      const int64_t i = perm[k];
+      if (i < 0 || i >= n) {
+        bad = 1;
+        break;
+      }
+      sz += 4 + (uint64_t)rd32(recs.data() + at[i]);
+    }
+    part[t + 1] = sz;
+  }
+  if (bad) return fail(SCT_BAM_EIO, "the order holds an index outside 0..%lld", (long long)(n - 1));
+  for (int t = 0; t < T; t++) part[t + 1] += part[t];
+  std::vector<uint8_t> out(part[T]);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+    uint64_t o = part[t];
+    for (int64_t k = lo; k < hi; k++) {
+      const uint64_t len = 4 + (uint64_t)rd32(recs.data() + at[perm[k]]);
+      memcpy(out.data() + o, recs.data() + at[perm[k]], len);
+      o += len;
+    }
+  }
+  std::vector<uint8_t>().swap(recs);
+  std::vector<z_stream> zs(n_threads);
+  for (auto& z : zs) {
+    memset(&z, 0, sizeof(z));
+    deflateInit2(&z, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+  }
+  struct ZEnd {
+    std::vector<z_stream>& zs;
+    ~ZEnd() {
+      for (auto& z : zs) deflateEnd(&z);
+    }
+  } zend{zs};
+  FILE* f = fopen(out_path, "wb");
+  if (!f) return fail(SCT_BAM_EIO, "cannot create %s", out_path);
+  struct Closer {
+    FILE*& f;
+    ~Closer() {
+      if (f) fclose(f);
+    }
+  } closer{f};
+  // the header in its own members, as htslib writes it, then the records, then EOF
+  for (int pass = 0; pass < 2; pass++) {
+    const uint8_t* src = pass == 0 ? (const uint8_t*)header0.data() : out.data();
+    const size_t total = pass == 0 ? header0.size() : out.size();
+    const size_t np = (total + kBgzfMaxInput - 1) / kBgzfMaxInput;
+    std::vector<std::vector<uint8_t>> z(np);
+#pragma omp parallel for num_threads(n_threads) schedule(dynamic, 1) reduction(| : bad)
+    for (long k = 0; k < (long)np; k++) {
+      const size_t o = (size_t)k * kBgzfMaxInput;
+      if (!bgzf_block(src + o, std::min(kBgzfMaxInput, total - o), level, zs[omp_get_thread_num()], z[k])) bad = 1;
+    }
+    if (bad) return fail(SCT_BAM_EIO, "deflate failed");
+    for (size_t k = 0; k < np; k++)
+      if (fwrite(z[k].data(), 1, z[k].size(), f) != z[k].size()) return fail(SCT_BAM_EIO, "cannot write %s", out_path);
+  }
+  if (fwrite(kBgzfEof, 1, sizeof(kBgzfEof), f) != sizeof(kBgzfEof)) return fail(SCT_BAM_EIO, "cannot write %s", out_path);
+  FILE* g = f;
+  f = nullptr;
+  if (fclose(g) != 0) return fail(SCT_BAM_EIO, "cannot close %s", out_path);
+  return SCT_BAM_OK;
+}
+
 }  // extern "C"

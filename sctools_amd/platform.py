@@ -9,6 +9,8 @@ codes as the reference's ``GenericPlatform`` metric commands
   MergeCellMetrics FILES... -o STEM
   MergeGeneMetrics FILES... -o STEM
   SplitBam -b BAM... -p PREFIX -t TAG... [-s MB] [--num-processes N] [--drop-missing]  (platform.py:153-223)
+  TagSortBam -i BAM -o BAM [-t TAG...]...                               (platform.py:60-97)
+  VerifyBamSort -i BAM [-t TAG...]...                                   (platform.py:100-143)
   CreateCountMatrix -b BAM -o PREFIX -a GTF [-c TAG -m TAG -g TAG -n]   (platform.py:384-470)
   MergeCountMatrices -i PREFIX... -o STEM                              (platform.py:475-516)
 
@@ -118,6 +120,41 @@ class GenericPlatform:
         return 0
 
     @classmethod
+    def tag_sort_bam(cls, args: Iterable[str] = None) -> int:
+        """TagSortBam (platform.py:60-97): the BAM sorted by the tags (zero or more), then the query
+        name; the order is computed on the GPU, the records are rewritten natively."""
+        parser = argparse.ArgumentParser(description="Sorts bam by list of zero or more tags, followed by query name")
+        parser.add_argument("-i", "--input_bam", required=True, help="input bamfile")
+        parser.add_argument("-o", "--output_bam", required=True, help="output bamfile")
+        parser.add_argument("-t", "--tags", nargs="+", action="append",
+                            help="tag(s) to sort by, separated by space, e.g. -t CB GE UB")
+        parser.add_argument("--device", default=None, help="torch device (default: current GPU)")
+        args = parser.parse_args(args) if args is not None else parser.parse_args()
+        bam.tag_sort_bam(args.input_bam, args.output_bam, cls.get_tags(args.tags), device=args.device)
+        return 0
+
+    @classmethod
+    def verify_bam_sort(cls, args: Iterable[str] = None) -> int:
+        """VerifyBamSort (platform.py:100-143): raises bam.SortError unless the BAM is sorted by
+        the tags (zero or more), then the query name; the check runs on the GPU."""
+        parser = argparse.ArgumentParser(
+            description="Verifies whether bam is sorted by the list of zero or more tags, followed by query name")
+        parser.add_argument("-i", "--input_bam", required=True, help="input bamfile")
+        parser.add_argument("-t", "--tags", nargs="+", action="append",
+                            help="tag(s) to use to verify sorting, separated by space, e.g. -t CB GE UB")
+        parser.add_argument("--device", default=None, help="torch device (default: current GPU)")
+        args = parser.parse_args(args) if args is not None else parser.parse_args()
+        tags = cls.get_tags(args.tags)
+        bam.verify_bam_sort(args.input_bam, tags, device=args.device)
+        print("{0} is correctly sorted by {1} and query name".format(args.input_bam, tags))
+        return 0
+
+    @classmethod
+    def get_tags(cls, raw_tags) -> list:
+        """-t A B -t C -> [A, B, C] (platform.py:145-150)."""
+        return [t for group in (raw_tags or []) for t in group]
+
+    @classmethod
     def bam_to_count_matrix(cls, args: Iterable[str] = None) -> int:
         """CreateCountMatrix (platform.py:384-470): query-name-grouped tagged BAM -> CSR count matrix."""
         parser = argparse.ArgumentParser()
@@ -171,6 +208,8 @@ COMMANDS = {
     "MergeCellMetrics": GenericPlatform.merge_cell_metrics,
     "MergeGeneMetrics": GenericPlatform.merge_gene_metrics,
     "SplitBam": GenericPlatform.split_bam,
+    "TagSortBam": GenericPlatform.tag_sort_bam,
+    "VerifyBamSort": GenericPlatform.verify_bam_sort,
     "CreateCountMatrix": GenericPlatform.bam_to_count_matrix,
     "MergeCountMatrices": GenericPlatform.merge_count_matrices,
 }
