@@ -110,31 +110,30 @@ struct EmitIn {
   }
 };
 
-// One block per kEmitTile records (input order, coalesced).  (1) rank every record among the
-// block's records of its gene bucket (one LDS atomic per record: measured faster than ranks
-// aggregated per wave with ballots, 0.64 vs 0.68 ms at config 2, hot bucket included);
-// (2) reserve one range per present bucket with one atomic on the bucket's cursor (k_gene_plan
-// set it to the bucket's start); (3) re-read the columns, build the payloads and write each at
-// its range + rank.
-// Each lane takes kEmitVec consecutive records per round, so every column is read with one
-// 4- to 16-byte load per lane (a wave covers 256 consecutive records per load); the ranks of
-// the lanes' k-th records are consecutive within a bucket, so the payload stores of one k
-// coalesce.  The order inside a bucket region is arbitrary; the reduction is order-free.
+// One block per kEmitTile records (input order, coalesced).  (1) count the block's records per
+// gene bucket (LDS atomics); (2) reserve one range per present bucket with one atomic on the
+// bucket's cursor (k_gene_plan set it to the bucket's start); (3) re-read the columns, rank
+// each record again within its bucket (a second LDS atomic: any order inside a range is fine,
+// the reduction is order-free) and write its payload at range + rank.  No per-record rank is
+// stored, so the tile can be large: a block's run per bucket is long and its payload stores
+// leave few partly written lines behind.  Each lane takes kEmitVec consecutive records per
+// round, so every column is read with one 4- to 16-byte load per lane (a wave covers 256
+// consecutive records per load); same-bucket lanes of one store get consecutive ranks (LDS
+// atomics on one address return in lane order), so the stores coalesce.
 constexpr int kEmitTile = 4 * kTile;
 constexpr int kEmitRounds = kEmitTile / (kBlock * kEmitVec);
 constexpr int kEmitBatch = 8;  // rounds whose gene loads are in flight together in pass 1
-static_assert(kEmitTile <= 65536, "ranks are 16-bit");
 static_assert(kEmitRounds % kEmitBatch == 0, "whole batches");
 
 template <bool kFull, bool k8>
 __device__ __forceinline__ void gene_emit_tile(const int32_t* __restrict__ gene, const RecCols& r,
                                                const uint16_t* __restrict__ dflags, int64_t n, int64_t base,
                                                uint32_t* __restrict__ cursor, int n_buckets, void* __restrict__ pay,
-                                               uint32_t* s_cnt, uint32_t* s_off, uint16_t* s_rank) {
+                                               uint32_t* s_cnt, uint32_t* s_off) {
   const int t = threadIdx.x;
   for (int i = t; i < n_buckets; i += kBlock) s_cnt[i] = 0;
   __syncthreads();
-  // (1) ranks: a batch of rounds' gene vectors loaded together, then ranked
+  // (1) counts: a batch of rounds' gene vectors loaded together, then counted
   for (int j0 = 0; j0 < kEmitRounds; j0 += kEmitBatch) {
     int32_t g[kEmitBatch][kEmitVec];
 #pragma unroll
@@ -142,21 +141,17 @@ __device__ __forceinline__ void gene_emit_tile(const int32_t* __restrict__ gene,
 #pragma unroll
     for (int b = 0; b < kEmitBatch; b++) {
       const int q0 = ((j0 + b) * kBlock + t) * kEmitVec;
-      uint32_t rk[kEmitVec];
 #pragma unroll
-      for (int k = 0; k < kEmitVec; k++) {
-        const bool valid = kFull || base + q0 + k < n;
-        const uint32_t bk = valid ? (uint32_t)g[b][k] / kGenesPerBucket : 0u;
-        rk[k] = valid ? atomicAdd(&s_cnt[bk], 1u) : 0u;
-      }
-      *reinterpret_cast<uint2*>(&s_rank[q0]) = make_uint2(rk[0] | (rk[1] << 16), rk[2] | (rk[3] << 16));
+      for (int k = 0; k < kEmitVec; k++)
+        if (kFull || base + q0 + k < n) atomicAdd(&s_cnt[(uint32_t)g[b][k] / kGenesPerBucket], 1u);
     }
   }
   __syncthreads();
-  // (2) one range per present bucket
+  // (2) one range per present bucket; the counters restart for the ranks of pass 3
   for (int i = t; i < n_buckets; i += kBlock) {
     const uint32_t c = s_cnt[i];
     if (c) s_off[i] = atomicAdd(&cursor[i], c);
+    s_cnt[i] = 0;
   }
   __syncthreads();
   // (3) payloads, software-pipelined: round j + 1's column loads are issued before round j's
@@ -169,14 +164,13 @@ __device__ __forceinline__ void gene_emit_tile(const int32_t* __restrict__ gene,
     const int64_t p0 = base + q0;
     EmitIn nxt;
     if (j + 1 < kEmitRounds) nxt.load<kFull>(gene, r, dflags, p0 + kBlock * kEmitVec, n);
-    const uint2 rp = *reinterpret_cast<const uint2*>(&s_rank[q0]);
-    const uint32_t rk[kEmitVec] = {rp.x & 0xffffu, rp.x >> 16, rp.y & 0xffffu, rp.y >> 16};
 #pragma unroll
     for (int k = 0; k < kEmitVec; k++) {
       if (kFull || p0 + k < n) {
         const uint32_t gk = (uint32_t)cur.g[k];
+        const uint32_t bk = gk / kGenesPerBucket;
         const uint32_t f = gene_flags(cur.bt[k], cur.xf[k], cur.df[k]);
-        const uint64_t at = (uint64_t)s_off[gk / kGenesPerBucket] + rk[k];
+        const uint64_t at = (uint64_t)s_off[bk] + atomicAdd(&s_cnt[bk], 1u);
         if constexpr (k8)
           reinterpret_cast<uint64_t*>(pay)[at] = gene_payload8(gk, f, cur.ug[k], cur.ul[k], cur.gg[k], cur.gl[k],
                                                                cur.gs[k]);
@@ -195,15 +189,14 @@ __global__ void __launch_bounds__(kBlock) k_gene_emit(const int32_t* __restrict_
                                                       const uint32_t* __restrict__ gwide, void* __restrict__ pay) {
   uint32_t* s_cnt = sct_dyn_lds;              // n_buckets (dynamic LDS)
   uint32_t* s_off = sct_dyn_lds + n_buckets;  // n_buckets
-  __shared__ __attribute__((aligned(16))) uint16_t s_rank[kEmitTile];
   const int64_t base = (int64_t)blockIdx.x * kEmitTile;
   const bool full = base + kEmitTile <= n, wide = *gwide != 0;  // block-uniform
   if (wide) {
-    if (full) gene_emit_tile<true, false>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
-    else gene_emit_tile<false, false>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
+    if (full) gene_emit_tile<true, false>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off);
+    else gene_emit_tile<false, false>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off);
   } else {
-    if (full) gene_emit_tile<true, true>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
-    else gene_emit_tile<false, true>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off, s_rank);
+    if (full) gene_emit_tile<true, true>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off);
+    else gene_emit_tile<false, true>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off);
   }
 }
 
