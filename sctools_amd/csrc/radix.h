@@ -27,7 +27,8 @@ __global__ void k_radix_upsweep(const uint64_t* __restrict__ keys, int64_t n, in
   const int wid = threadIdx.x / kWave;
   for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&hist[0][0])[i] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  const unsigned tile = xcd_tile(blockIdx.x, gridDim.x);  // consecutive tiles on one XCD
+  const int64_t base = (int64_t)tile * kSortTile;
 #pragma unroll
   for (int j = 0; j < kSortItems; j++) {
     const int64_t p = base + (int64_t)j * kBlock + threadIdx.x;
@@ -38,7 +39,7 @@ __global__ void k_radix_upsweep(const uint64_t* __restrict__ keys, int64_t n, in
     uint32_t t = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; w++) t += hist[w][d];
-    counts[(int64_t)d * num_tiles + blockIdx.x] = t;
+    counts[(int64_t)d * num_tiles + tile] = t;
   }
 }
 
@@ -56,11 +57,14 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __re
 
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  // consecutive tiles on one XCD: a digit's runs of neighbouring tiles are neighbours in the
+  // output, so their partly written lines meet in that XCD's L2 instead of two L2s
+  const unsigned tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t base = (int64_t)tile * kSortTile;
   const int tile_n = (int)((n - base) < kSortTile ? (n - base) : kSortTile);
 
   for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_whist[0][0])[i] = 0;
-  s_goff[threadIdx.x] = offsets[(int64_t)threadIdx.x * num_tiles + blockIdx.x];  // kRadix == kBlock
+  s_goff[threadIdx.x] = offsets[(int64_t)threadIdx.x * num_tiles + tile];  // kRadix == kBlock
   __syncthreads();
 
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));

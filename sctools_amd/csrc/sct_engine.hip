@@ -791,9 +791,13 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
     rk.nf = nf - 1;
     rk.bits = field_bits;
     for (int i = 0; i < rk.nf; i++) rk.f[i] = f[i];
-    LAUNCH("tag_keys", k_field_keys, grid, dim3(kBlock), s, *in, n, rk, B.ka, B.va);
+    const int tie_top = f[nf - 1].bits;  // the tiebreak's width
+    int th = (field_bits + kRadixBits - 1) / kRadixBits * kRadixBits - field_bits;  // free bits of the last digit
+    if (th > tie_top) th = tie_top;
+    if (field_bits + th > 64) th = 64 - field_bits;
+    LAUNCH("tag_keys", k_field_keys, grid, dim3(kBlock), s, *in, n, rk, tiebreak, tie_top, th, B.ka, B.va);
     int which = 0;
-    rc = radix_sort(B, n, field_bits, &which, s);
+    rc = radix_sort(B, n, field_bits + th, &which, s);
     if (rc) return rc;
     const uint64_t* keys = which ? B.kb : B.ka;
     uint32_t* perm = which ? B.vb : B.va;

@@ -128,7 +128,8 @@ __global__ void __launch_bounds__(kBlock) k_row_hist(const int32_t* __restrict__
   const int wid = threadIdx.x / kWave;
   for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&hist[0][0])[i] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kRowTile;
+  const unsigned tile = xcd_tile(blockIdx.x, gridDim.x);  // consecutive tiles on one XCD (radix.h)
+  const int64_t base = (int64_t)tile * kRowTile;
 #pragma unroll
   for (int j = 0; j < kRowItems; j++) {
     const int64_t p = base + (int64_t)j * kBlock + threadIdx.x;
@@ -139,7 +140,7 @@ __global__ void __launch_bounds__(kBlock) k_row_hist(const int32_t* __restrict__
   uint32_t t = 0;
 #pragma unroll
   for (int w = 0; w < kWaves; w++) t += hist[w][d];
-  counts[(int64_t)d * tiles + blockIdx.x] = t;
+  counts[(int64_t)d * tiles + tile] = t;
 }
 
 template <bool kFromSoA, bool kToSoA>
@@ -154,10 +155,11 @@ __global__ void __launch_bounds__(kBlock) k_row_scatter(sct_records_t in, const 
   __shared__ uint64_t s_scan[kWaves + 1];
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
-  const int64_t base = (int64_t)blockIdx.x * kRowTile;
+  const unsigned tile = xcd_tile(blockIdx.x, gridDim.x);  // consecutive tiles on one XCD (radix.h)
+  const int64_t base = (int64_t)tile * kRowTile;
   const int tile_n = (int)((n - base) < kRowTile ? (n - base) : kRowTile);
   for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_whist[0][0])[i] = 0;
-  s_goff[threadIdx.x] = offsets[(int64_t)threadIdx.x * tiles + blockIdx.x];
+  s_goff[threadIdx.x] = offsets[(int64_t)threadIdx.x * tiles + tile];
   __syncthreads();
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
   uint4 ra[kRowItems], rb[kRowItems];
@@ -264,7 +266,12 @@ __global__ void __launch_bounds__(kBlock) k_row_scatter(sct_records_t in, const 
 // round (27 query-name bits) and the gather of its keys.
 constexpr int kTieShort = 16;
 
+// The field key of every record in input order, followed by the top `th` bits of its tiebreak
+// (tie_bits wide): the bits the last radix digit has free past the fields cost no pass, and they
+// split most runs of equal fields (duplicates rarely share their query-name rank's top bits), so
+// the run fix-up gathers the full tiebreak for far fewer records.
 __global__ void __launch_bounds__(kBlock) k_field_keys(sct_records_t r, int64_t n, RoundKey rk,
+                                                       const int32_t* __restrict__ tie, int tie_bits, int th,
                                                        uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
@@ -275,6 +282,7 @@ __global__ void __launch_bounds__(kBlock) k_field_keys(sct_records_t r, int64_t 
     const uint64_t v = (uint64_t)f[rk.f[i].which] & (b >= 32 ? 0xFFFFFFFFull : ((1ull << b) - 1));
     k = b ? ((b >= 64 ? 0ull : (k << b)) | v) : k;
   }
+  if (th > 0) k = (k << th) | (((uint32_t)tie[j] >> (tie_bits - th)) & ((1u << th) - 1));
   keys[j] = k;
   vals[j] = (uint32_t)j;
 }
