@@ -332,8 +332,9 @@ struct GeneAcc {
     pk[0] += spread_bytes(g.f & 0xffu);
     pk[1] += spread_bytes(g.f >> 8);
     fx_accumulate(l + 0 * kStreamLanes, ratio_rcp(g.ua, g.ub, s_rcp));
-    fx_accumulate(l + 1 * kStreamLanes, ratio_rcp(g.qa, g.qb, s_rcp));
-    fx_accumulate(l + 2 * kStreamLanes, ratio_rcp(g.qs, g.qb, s_rcp));
+    const double yq = rcp_of(g.qb, s_rcp);  // the two gq quotients share the reciprocal
+    fx_accumulate(l + 1 * kStreamLanes, ratio_y(g.qa, g.qb, yq));
+    fx_accumulate(l + 2 * kStreamLanes, ratio_y(g.qs, g.qb, yq));
   }
   __device__ __forceinline__ int32_t byte(int f) const { return (int32_t)((pk[f / 8] >> (8 * (f % 8))) & 0xffu); }
   // unconditional adds (zeros included): a per-lane test would cost an exec-mask round per lane

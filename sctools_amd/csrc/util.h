@@ -246,13 +246,19 @@ constexpr int kRcpN = 256;  // table of 1/b for b < kRcpN (LDS); larger b divide
 __device__ __forceinline__ void fill_rcp(double* s_rcp) {
   for (int i = threadIdx.x; i < kRcpN; i += blockDim.x) s_rcp[i] = i ? 1.0 / (double)i : 0.0;
 }
-__device__ __forceinline__ double ratio_rcp(uint32_t a, uint32_t b, const double* s_rcp) {
-  if (b == 0) return 0.0;
-  const double y = b < (uint32_t)kRcpN ? s_rcp[b] : 1.0 / (double)b;
+__device__ __forceinline__ double rcp_of(uint32_t b, const double* s_rcp) {  // RN(1 / b); 0 for b == 0
+  return b < (uint32_t)kRcpN ? s_rcp[b] : 1.0 / (double)b;
+}
+// RN(a / b) from y = RN(1 / b); 0 when y == 0 (b == 0: the table's entry 0)
+__device__ __forceinline__ double ratio_y(uint32_t a, uint32_t b, double y) {
   const double da = (double)a, db = (double)b;
   const double q0 = da * y;
   const double r = __fma_rn(-q0, db, da);
   return __fma_rn(r, y, q0);
+}
+__device__ __forceinline__ double ratio_rcp(uint32_t a, uint32_t b, const double* s_rcp) {
+  if (b == 0) return 0.0;
+  return ratio_y(a, b, rcp_of(b, s_rcp));
 }
 
 __device__ __forceinline__ uint32_t frag_hash(int32_t ref, int32_t pos, uint32_t strand) {
