@@ -187,7 +187,8 @@ int launch_hash_tile(bool cell, bool gene, dim3 grid, hipStream_t s, const uint1
 }
 
 // bucket.h driver: level 0 classification, MSD levels until no segment exceeds kBCap, then
-// the hash-tile pass (+ giants).  One host sync per level to size the next level's launches.
+// the hash-tile pass (+ giants).  One host wait per level to size the next level's launches,
+// for a copy queued right after the classification: the level's scatter runs meanwhile.
 // Returns 1 (not an error code) when build_keys saw a mapped ref id the payload cannot hold:
 // the caller then reruns on the global-sort path.
 int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const int64_t* ent_start,
@@ -236,9 +237,12 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     LAUNCH("bucket_classify", k_bucket_classify, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c],
            (const uint32_t*)hist, cur, depth, bits, b.k1, b.k1 + b.k2, KB, level & 1, bdesc, bent, seg[c ^ 1],
            work[c ^ 1], giants, bigs, ctl);
-    LAUNCH("bucket_scatter", k_bucket_scatter, dim3(h.n_work), dim3(kBlock), s, kin, vin, kout, vout,
+    // the next level's counts are final after classify: read them while the scatter runs
+    if (int rb = readback_start(ctl, sizeof(h), s)) return rb;
+    const uint32_t n_work = h.n_work;
+    LAUNCH("bucket_scatter", k_bucket_scatter, dim3(n_work), dim3(kBlock), s, kin, vin, kout, vout,
            (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
-    if (int rb = readback(&h, ctl, sizeof(h), s)) return rb;
+    if (int rb = readback_finish(&h, sizeof(h))) return rb;
     c ^= 1;
     depth += bits;
     level++;

@@ -66,6 +66,38 @@ inline int readback(void* dst, const void* src, size_t bytes, hipStream_t s) {
   return SCT_OK;
 }
 
+// The same readback split in two: the copy is queued (readback_start) and waited for later
+// (readback_finish), so the kernels queued in between keep the device busy while the host
+// waits for the copy.  One outstanding early readback per host thread.
+struct EarlyReadback {
+  void* buf = nullptr;
+  hipEvent_t ev = nullptr;
+  ~EarlyReadback() {
+    if (buf) (void)hipHostFree(buf);
+    if (ev) (void)hipEventDestroy(ev);
+  }
+};
+inline EarlyReadback& early_readback() {
+  static thread_local EarlyReadback rb;
+  return rb;
+}
+inline int readback_start(const void* src, size_t bytes, hipStream_t s) {
+  EarlyReadback& rb = early_readback();
+  if (bytes > PinnedReadback::kCap)
+    return fail(SCT_EINVAL, "readback of %zu bytes exceeds %zu", bytes, PinnedReadback::kCap);
+  if (!rb.buf) HIPCHK(hipHostMalloc(&rb.buf, PinnedReadback::kCap, hipHostMallocPortable));
+  if (!rb.ev) HIPCHK(hipEventCreateWithFlags(&rb.ev, hipEventDisableTiming));
+  HIPCHK(hipMemcpyAsync(rb.buf, src, bytes, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(rb.ev, s));
+  return SCT_OK;
+}
+inline int readback_finish(void* dst, size_t bytes) {
+  EarlyReadback& rb = early_readback();
+  HIPCHK(hipEventSynchronize(rb.ev));
+  memcpy(dst, rb.buf, bytes);
+  return SCT_OK;
+}
+
 // ---------------- host: optional per-kernel timing with HIP events ----------------
 struct ProfEntry {
   std::string name;
