@@ -189,3 +189,26 @@ def test_tag_sort_bam_is_the_stable_sort(tmp_path, tags):
     _, got = raw_records(out)
     assert got == [raw[i] for i in stable]  # sorted() is stable: ties keep input order
     assert host_verdict(out, tags) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tags", [["CB", "UB", "GE"], ["GE", "CB"], []], ids=["CB-UB-GE", "GE-CB", "none"])
+def test_tag_sort_bam_on_a_shuffled_13k_record_file(tmp_path, tags):
+    """cell-sorted-missing-cb.bam (13,236 records, CB missing on some, secondaries sharing query
+    names) shuffled by the native writer, then TagSortBam: the records in exactly the order of
+    Python's stable sort of the shuffled file; VerifyBamSort accepts the output and rejects the
+    shuffled input."""
+    src = bam_path("cell-sorted-missing-cb")
+    _, raw = raw_records(src)
+    shuffled = str(tmp_path / "shuffled.bam")
+    BN.write_order(src, shuffled, np.random.default_rng(7).permutation(len(raw)))
+    out = str(tmp_path / "sorted.bam")
+    B.tag_sort_bam(shuffled, out, tags)
+    _, sraw = raw_records(shuffled)
+    py = list(B.open_alignments(shuffled, "rb"))
+    stable = sorted(range(len(py)), key=lambda i: B.TagSortableRecord.from_aligned_segment(py[i], tags))
+    _, got = raw_records(out)
+    assert got == [sraw[i] for i in stable]
+    B.verify_bam_sort(out, tags)
+    with pytest.raises(B.SortError):
+        B.verify_bam_sort(shuffled, tags)
