@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define SCT_ABI_VERSION 1
+#define SCT_ABI_VERSION 2
 
 /* ---- error codes ---- */
 #define SCT_OK 0
@@ -291,6 +291,7 @@ typedef struct sct_count_output {
   int64_t nnz;        /* host, set on return */
   int64_t unknown_record; /* host: first record (file order) of a counted molecule whose gene is
                            * SCT_COUNT_UNKNOWN -- the reference's KeyError -- or -1 */
+  int64_t n_sorted;       /* host: molecule keys sorted (the counted query-name groups) */
 } sct_count_output_t;
 
 /* Device workspace bytes for sct_count_matrix. */

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SCT_LIB_PATH") or os.path.join(HERE, "libsctools_gpu.so")  # override: experiments only
 
-SCT_ABI_VERSION = 1
+SCT_ABI_VERSION = 2
 SCT_NI, SCT_NF, SCT_NP = 24, 12, 64
 SCT_P_FLOAT_BASE, SCT_P_STREAM_LANES = 24, 8
 
@@ -89,6 +89,7 @@ class CountOutput(ctypes.Structure):
         ("n_rows", ctypes.c_int64),
         ("nnz", ctypes.c_int64),
         ("unknown_record", ctypes.c_int64),
+        ("n_sorted", ctypes.c_int64),
     ]
 
 

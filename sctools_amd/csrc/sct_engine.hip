@@ -887,7 +887,7 @@ int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void*
                      void* stream) {
   last_error().clear();
   if (!in || !out) return fail(SCT_EINVAL, "NULL argument");
-  out->n_rows = out->nnz = 0;
+  out->n_rows = out->nnz = out->n_sorted = 0;
   out->unknown_record = -1;
   const int64_t n = in->n;
   if (n < 0 || n >= (int64_t)0x7FFFFFFF) return fail(SCT_EINVAL, "records must be in [0, 2^31 - 1)");
@@ -951,6 +951,7 @@ int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void*
     return SCT_OK;
   }
   const int64_t m = (int64_t)h[1];
+  out->n_sorted = m;
   int64_t nnz = 0, n_rows = 0;
   uint64_t n_triples = 0;
   if (m > 0) {

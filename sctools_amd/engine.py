@@ -252,6 +252,7 @@ class Engine:
         N.check(self.lib.sct_count_matrix(ctypes.byref(ci), ctypes.byref(co), ctypes.c_void_p(ws.data_ptr()),
                                           ws.numel(), self._stream()))
         del ws
+        self.count_stats = {"sorted": int(co.n_sorted), "rows": int(co.n_rows), "nnz": int(co.nnz)}
         if co.unknown_record >= 0:
             return None, int(co.unknown_record)
         r, z = int(co.n_rows), int(co.nnz)

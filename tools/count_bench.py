@@ -78,7 +78,17 @@ def main():
     dom = max(kms, key=kms.get)
     launches = prof[dom][1] / args.steps
     per_launch_ms = kms[dom] / launches
-    achieved = ALG.get(dom, 0) * n / (per_launch_ms * 1e-3) / 1e9
+    # the radix kernels sort the counted groups' molecule keys (eng.count_stats["sorted"] items,
+    # cbits + colbits + ubits bits) and then the rows' (first record, cell) keys (rows items,
+    # 32 bits): algorithmic bytes per step over the kernel's total time per step
+    sorted_items = eng.count_stats["sorted"]
+    bitlen = lambda v: max(0, int(v - 1).bit_length())  # noqa: E731
+    mol_passes = -(-(bitlen(nc) + bitlen(ng) + bitlen(1 << 20)) // 8)
+    row_passes = int(round(launches)) - mol_passes
+    items = {"radix_downsweep": sorted_items * mol_passes + int(res[0].numel()) * row_passes,
+             "radix_upsweep": sorted_items * mol_passes + int(res[0].numel()) * row_passes}
+    step_bytes = ALG.get(dom, 0) * items.get(dom, n * launches)
+    achieved = step_bytes / (kms[dom] * 1e-3) / 1e9
     # CPU baseline: the oracle's column restatement, one core, on a leading sample
     from oracle import count_oracle as O
 
@@ -99,7 +109,8 @@ def main():
                    "rows": int(res[0].numel()), "nnz": nnz},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                      "frac": achieved / 8000.0, "avg_launch_ms": per_launch_ms, "launches_per_step": launches,
-                     "alg_bytes_per_record": ALG.get(dom, 0)},
+                     "alg_bytes_per_item": ALG.get(dom, 0), "items_per_step": items.get(dom, n * launches),
+                     "sorted_molecule_keys": sorted_items},
         "kernel_ms_per_step": {k: round(v, 4) for k, v in kms.items()},
         "cpu_baseline": {"value": m / cpu_s, "unit": "records/s", "cores": 1, "kind": "port",
                          "sample": "first %d records: oracle count_columns loop, %.1fs" % (m, cpu_s)},
