@@ -11,6 +11,7 @@
 // lanes of the quality streams (fixedpt.h).  Runs are contiguous in input order, so
 // a thread flushes once per run it touches and a wave once per tile.
 #pragma once
+#include <type_traits>
 #include "bucket.h"
 #include "fixedpt.h"
 #include "radix.h"
@@ -130,73 +131,132 @@ struct AddAcc {
   }
 };
 
-// s_e holds one int per tile position with one pad word after every 16: the blocked passes
-// (thread t reads positions 16t .. 16t+15) then hit distinct banks instead of 16-way conflicts.
-__device__ __forceinline__ int epad(int q) { return q + (q >> 4); }
+// s_e16 holds, per tile position, the run index relative to the run before the tile's first
+// head (local 0 = the run continuing from the previous tile), two pad halves after every 32: the
+// blocked passes (thread t reads positions 32t .. 32t+31, 17 words apart) then hit distinct banks.
+__device__ __forceinline__ int epad(int q) { return q + 2 * (q >> 5); }
 // The key pass (k_build_keys_run) owns kKTile records per block, kKItems per thread: twice the
 // heads tile (k_heads / tile offsets are per kTile), which halves the per-block costs (run-id
 // scan, the wave flushes that end each quality stream, the gene-bucket histogram flush).
 constexpr int kKItems = 2 * kItems;  // 32: the blocked head masks are 32-bit
 constexpr int kKTile = kBlock * kKItems;
 constexpr int kKTilesPerBlock = kKTile / kTile;
-constexpr int kTilePad = kKTile + kKTile / 16;
+constexpr int kTilePad = kKTile + 2 * (kKTile / 32);
+constexpr int kRunBatch = 8;  // striped rounds whose entity loads are in flight together
 static_assert(kKItems <= 32, "head masks are 32-bit");
+static_assert(kKItems % kRunBatch == 0, "whole batches");
+static_assert(kKTile <= 65535, "local run ids are 16-bit");
 
-// Stage the tile's entity column, find run heads, and number the runs: s_e[epad(q)] = run index of
-// tile position q.  Writes ent_start[run] for heads when ent_start is set.  Block-wide (barriers).
-__device__ __forceinline__ void tile_run_ids(const int32_t* __restrict__ ent, int64_t n, int64_t base, int tile_n,
-                                             uint64_t tile_off, int32_t* s_e, int32_t* s_prev, uint64_t* s_scan,
-                                             int64_t* __restrict__ ent_start) {
-  const int t = threadIdx.x;
-#pragma unroll 4
-  for (int j = 0; j < kKItems; j++) {
-    const int q = j * kBlock + t;
-    if (q < tile_n) s_e[epad(q)] = ent[base + q];
-  }
-  if (t == 0) *s_prev = base > 0 ? ent[base - 1] : 0;
-  __syncthreads();
-  const int q0 = t * kKItems;
-  uint32_t heads = 0;
-  {
-    int32_t prev = q0 > 0 ? s_e[epad(q0 - 1)] : *s_prev;
+// Number the runs of the tile: s_e16[epad(q)] = run index of tile position q minus the returned
+// base (tile_off - 1).  Heads are found on striped, coalesced loads (the previous record comes
+// from the neighbouring lane; lane 0 re-reads it, a cache hit) and kept as one bit per position
+// (s_hb: kKTile / 64 words, ballots); each thread then numbers its 32 blocked positions from its
+// word of the mask and a block scan.  Writes ent_start[run] for heads when ent_start is set.
+// Block-wide (barriers).
+// Also returns the thread's blocked head mask (*my_heads) and the local id of the run before its
+// first position (*my_ex): the run of position 32t + j is ebase + my_ex + popc(heads & bits 0..j).
+__device__ __forceinline__ int64_t tile_run_ids(const int32_t* __restrict__ ent, int64_t base, int tile_n,
+                                                uint64_t tile_off, uint16_t* s_e16, uint64_t* s_hb,
+                                                uint64_t* s_scan, int64_t* __restrict__ ent_start,
+                                                uint32_t* my_heads, uint32_t* my_ex) {
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  for (int j0 = 0; j0 < kKItems; j0 += kRunBatch) {
+    int32_t v[kRunBatch], pv[kRunBatch];
 #pragma unroll
-    for (int j = 0; j < kKItems; j++) {
-      const int q = q0 + j;
-      if (q < tile_n) {
-        const int32_t v = s_e[epad(q)];
-        const bool h = (base + q == 0) || v != prev;
-        heads |= (h ? 1u : 0u) << j;
-        prev = v;
-      }
+    for (int u = 0; u < kRunBatch; u++) {
+      const int q = (j0 + u) * kBlock + t;
+      const int64_t p = base + (q < tile_n ? q : 0);
+      v[u] = ent[p];
+      pv[u] = (lane == 0 && p > 0) ? ent[p - 1] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kRunBatch; u++) {
+      const int q = (j0 + u) * kBlock + t;
+      const int32_t up = __shfl_up(v[u], 1);
+      const int32_t prev = lane == 0 ? pv[u] : up;
+      const bool h = q < tile_n && (base + q == 0 || v[u] != prev);
+      const uint64_t m = __ballot(h);
+      if (lane == 0) s_hb[(j0 + u) * kWaves + w] = m;  // positions 64 ((j0 + u) kWaves + w) + [0, 64)
     }
   }
+  __syncthreads();
+  const uint32_t heads = reinterpret_cast<const uint32_t*>(s_hb)[t];  // blocked positions 32t .. 32t+31
   uint64_t tot;
   const uint64_t ex = block_exclusive_scan<uint64_t>((uint64_t)__popc(heads), &tot, s_scan);  // has barriers
-  int64_t e = (int64_t)(tile_off + ex) - 1;
+  const int64_t ebase = (int64_t)tile_off - 1;
+  *my_heads = heads;
+  *my_ex = (uint32_t)ex;
+  uint32_t loc = (uint32_t)ex;
+  const int q0 = t * kKItems;
+  uint32_t* s_w = reinterpret_cast<uint32_t*>(s_e16);
 #pragma unroll
-  for (int j = 0; j < kKItems; j++) {
-    const int q = q0 + j;
-    if (q >= tile_n) break;
-    if (heads & (1u << j)) {
-      e += 1;
-      if (ent_start) ent_start[e] = base + q;
+  for (int j = 0; j < kKItems; j += 2) {  // two positions per 32-bit store (epad(q0 + j) is even)
+    uint32_t l2[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      if ((heads >> (j + k)) & 1u) {
+        loc += 1;
+        if (ent_start) ent_start[ebase + loc] = base + q0 + j + k;
+      }
+      l2[k] = loc;
     }
-    s_e[epad(q)] = (int32_t)e;
+    if (q0 + j < tile_n) s_w[epad(q0 + j) / 2] = l2[0] | (l2[1] << 16);
   }
   __syncthreads();
+  return ebase;
 }
 
-// The exact fixed-point lanes of the quality streams for one tile whose run ids are in s_e
-// (tile_run_ids): blocked items (kItems consecutive records per thread) with 16-byte vector
-// loads; the streams are summed one after another so only 8 lanes are live per thread.
+// Exact-lane increments of RN(a / B) for one denominator B per barcode stream and tile (the tile's
+// first record's): a sample with that denominator adds 8 table words instead of computing them
+// (fx_increments).  Barcode lengths are fixed in a chemistry; any other denominator is computed
+// in place (a rare divergent branch).  Table entries are computed with the same ratio_y /
+// fx_increments as the computed samples, so the lanes are bit-identical either way.  The genomic
+// streams keep the arithmetic: soft-clipped reads change gq_len on ~1 record in 8, so a wave would
+// run both paths every round.
+constexpr int kTabU8 = 32;  // uy / cy (uint8 lengths): a = 0 .. 31
+constexpr int kTabN = 2 * kTabU8;
+constexpr uint32_t kNoTab = 0xffffffffu;
+struct StreamTabs {
+  uint4 inc[kTabN][2];  // the 8 lane increments of a (inc7 < 2^32: a <= B means x <= 1)
+  uint32_t den[2];      // per table (uy, cy): the tabulated denominator, or kNoTab
+};
+static_assert(kTabN <= kBlock, "one entry per thread");
+
+template <bool kCell>
+__device__ __forceinline__ void fill_stream_tabs(const RecCols& r, int64_t base, StreamTabs* s) {
+  const int t = threadIdx.x;
+  if (t >= kTabN) return;
+  const int tb = t / kTabU8;
+  const uint32_t a = (uint32_t)(t % kTabU8);
+  const uint32_t B = tb == 0 ? (uint32_t)r.uy_len[base] : (kCell ? (uint32_t)r.cy_len[base] : 0u);
+#ifndef SCT_TAB_MASK
+#define SCT_TAB_MASK 3  // experiments: which tables are used (bit 0 uy, bit 1 cy)
+#endif
+  const bool on = B < (uint32_t)kTabU8 && (kCell || tb == 0) && ((SCT_TAB_MASK >> tb) & 1);
+  if (a == 0) s->den[tb] = on ? B : kNoTab;
+  const double x = (on && B != 0 && a <= B) ? ratio_y(a, B, 1.0 / (double)B) : 0.0;  // = ratio_rcp(a, B)
+  uint32_t inc[kStreamLanes - 1];
+  uint64_t inc7;
+  fx_increments(x, inc, inc7);
+  s->inc[t][0] = make_uint4(inc[0], inc[1], inc[2], inc[3]);
+  s->inc[t][1] = make_uint4(inc[4], inc[5], inc[6], (uint32_t)inc7);
+}
+
+// The exact fixed-point lanes of the quality streams for one tile: blocked items (kItems
+// consecutive records per thread, two halves of the thread's kKItems) with 16-byte vector loads;
+// the streams are summed one after another so only 8 lanes are live per thread.  Runs come from
+// the thread's head mask (tile_run_ids: `heads`, `ex`), not from LDS: a half whose wave holds no
+// run boundary (almost all of them: runs are cells of thousands of records) sums its 16 samples
+// with no flush test at all.
 // gwide (gene view): set when an operand exceeds the narrow gene payload (gene.h gene_payload8).
 template <bool kCell>
-__device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int tile_n, const int32_t* s_e,
-                                            const double* s_rcp, int64_t* __restrict__ partials,
-                                            uint32_t* __restrict__ gwide) {
+__device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int tile_n, uint32_t heads, uint32_t ex,
+                                            int64_t ebase, const double* s_rcp, const StreamTabs* s_tab,
+                                            int64_t* __restrict__ partials, uint32_t* __restrict__ gwide) {
   const int t = threadIdx.x;
   constexpr int ns = kCell ? 4 : 3;
   // numerator / denominator columns of half h of stream st: items q0 .. q0 + kItems - 1 of the thread's kKItems
+  // (zeros past the tile: a zero sample adds nothing)
   const auto load = [&](int st, int h, uint32_t (&wn)[8], uint32_t (&wd)[8]) {
     const int q0 = t * kKItems + h * kItems;
     const int64_t p0 = base + q0;
@@ -238,6 +298,8 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
       }
     }
   };
+  // a thread with no position in the tile holds no run (its lanes stay zero and never flush)
+  const bool mine = t * kKItems < tile_n;
   int64_t lanes[kStreamLanes];
   int64_t cur_e = -1;
   // the next (stream, half)'s columns are loaded before the current one is summed (software
@@ -250,11 +312,10 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
     const int st = sh >> 1, h = sh & 1;
     const bool wide = (st == 1 || st == 2);
     if (sh + 1 < 2 * ns) load((sh + 1) >> 1, (sh + 1) & 1, nn, nd);
-    const int q0 = t * kKItems + h * kItems;
     if (h == 0) {
 #pragma unroll
       for (int i = 0; i < kStreamLanes; i++) lanes[i] = 0;
-      cur_e = -1;
+      cur_e = mine ? ebase + (int64_t)ex + (int64_t)(heads & 1u) : -1;  // the run of the thread's first position
     }
     {  // on the packed columns: uy (u8) above 31, gq_gt30 / gq_len (u16) above 511, gq_sum above 32767
       const uint32_t m = st == 0 ? 0xE0E0E0E0u : st == 1 ? 0xFE00FE00u : st == 2 ? 0x80008000u : 0u;
@@ -265,17 +326,34 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
     }
     const int slot0 = P_FLOAT + st * kStreamLanes;
     const auto slot = [slot0](int i) { return slot0 + i; };
-#pragma unroll
-    for (int j = 0; j < kItems; j++) {
-      const int q = q0 + j;
-      const bool valid = q < tile_n;
-      const int64_t e = valid ? (int64_t)s_e[epad(q)] : cur_e;
-      wave_flush<kStreamLanes>(lanes, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
-      if (!valid) continue;
-      cur_e = e;
+    const int tb = st == 0 ? 0 : st == 3 ? 1 : -1;
+    const uint32_t B = tb >= 0 ? s_tab->den[tb] : kNoTab;  // block-uniform
+    const uint4* tab = &s_tab->inc[tb >= 0 ? tb * kTabU8 : 0][0];
+    const auto sample = [&](int j) {
       const uint32_t a = wide ? (wn[j / 2] >> (16 * (j % 2))) & 0xffffu : (wn[j / 4] >> (8 * (j % 4))) & 0xffu;
       const uint32_t d = wide ? (wd[j / 2] >> (16 * (j % 2))) & 0xffffu : (wd[j / 4] >> (8 * (j % 4))) & 0xffu;
-      fx_accumulate(lanes, ratio_rcp(a, d, s_rcp));
+      if (B != kNoTab && d == B && a <= B) {
+        const uint4 i0 = tab[2 * a], i1 = tab[2 * a + 1];
+        lanes[0] += i0.x, lanes[1] += i0.y, lanes[2] += i0.z, lanes[3] += i0.w;
+        lanes[4] += i1.x, lanes[5] += i1.y, lanes[6] += i1.z, lanes[7] += i1.w;
+      } else {
+        fx_accumulate(lanes, ratio_rcp(a, d, s_rcp));
+      }
+    };
+    // run changes inside this half: head bits of its positions (the first position of the thread
+    // opened cur_e already)
+    const uint32_t ch = ((heads >> (h * kItems)) & ((1u << kItems) - 1u)) & (h == 0 ? ~1u : ~0u);
+    if (!__ballot(ch != 0)) {
+#pragma unroll
+      for (int j = 0; j < kItems; j++) sample(j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kItems; j++) {
+        const bool hd = (ch >> j) & 1u;
+        wave_flush<kStreamLanes>(lanes, hd, cur_e, partials, slot);
+        if (hd) cur_e += 1;
+        sample(j);
+      }
     }
     if (h == 1) wave_flush<kStreamLanes>(lanes, cur_e >= 0, cur_e, partials, slot);
 #pragma unroll
@@ -301,9 +379,12 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
                                                            uint32_t* __restrict__ gene_counts, int n_buckets,
                                                            uint32_t* __restrict__ err, uint32_t* __restrict__ gwide) {
   static_assert(!kGene || kCell, "gene buckets come from the cell view");
-  __shared__ int32_t s_e[kTilePad];
-  __shared__ int32_t s_prev;
+  __shared__ uint16_t s_e16[kTilePad];
   __shared__ uint64_t s_scan[kWaves + 1];
+  __shared__ uint64_t s_hb[kKTile / 64];  // tile_run_ids' head bits
+  using TabT = typename std::conditional<kStreams, StreamTabs, uint32_t>::type;
+  __shared__ TabT s_tab_[1];
+  StreamTabs* s_tab = reinterpret_cast<StreamTabs*>(s_tab_);
   uint32_t* s_hist = sct_dyn_lds;  // kGene: n_buckets counters (dynamic LDS)
   __shared__ double s_rcp[kStreams ? kRcpN : 1];
   const int t = threadIdx.x;
@@ -311,10 +392,14 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
   const int tile_n = (int)((n - base) < kKTile ? (n - base) : kKTile);
   if (kGene)
     for (int i = t; i < n_buckets; i += kBlock) s_hist[i] = 0;
-  if (kStreams) fill_rcp(s_rcp);  // visible after tile_run_ids' barriers
+  if constexpr (kStreams) {  // visible after tile_run_ids' barriers
+    fill_rcp(s_rcp);
+    fill_stream_tabs<kCell>(r, base, s_tab);
+  }
   // 1-2. run index of every record of the tile
-  tile_run_ids(c.ent, n, base, tile_n, tile_off[(size_t)blockIdx.x * kKTilesPerBlock], s_e, &s_prev, s_scan,
-               ent_start);
+  uint32_t my_heads, my_ex;
+  const int64_t ebase = tile_run_ids(c.ent, base, tile_n, tile_off[(size_t)blockIdx.x * kKTilesPerBlock], s_e16,
+                                     s_hb, s_scan, ent_start, &my_heads, &my_ex);
 
   // 3. striped pass: keys, values and the run's additive metrics.  Runs are contiguous, so
   // in a round the wave's lanes cross a run boundary together: flush wave-cooperatively.
@@ -344,7 +429,7 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
       const int q = (j0 + u) * kBlock + t;
       const bool valid = q < tile_n;
       const int64_t p = base + q;
-      const int64_t e = valid ? (int64_t)s_e[epad(q)] : cur_e;
+      const int64_t e = valid ? ebase + (int64_t)s_e16[epad(q)] : cur_e;
       wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
       if (!valid) continue;
       cur_e = e;
@@ -399,7 +484,8 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
     for (int i = t; i < n_buckets; i += kBlock)
       if (s_hist[i]) atomicAdd(&gene_counts[i], s_hist[i]);
   }
-  if constexpr (kStreams) stream_tile<kCell>(r, base, tile_n, s_e, s_rcp, partials, kGene ? gwide : nullptr);
+  if constexpr (kStreams) stream_tile<kCell>(r, base, tile_n, my_heads, my_ex, ebase, s_rcp, s_tab, partials,
+                                                 kGene ? gwide : nullptr);
 }
 
 }  // namespace sct
