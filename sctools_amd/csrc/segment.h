@@ -424,15 +424,33 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
       vref[u] = r.ref[p];
       vpos[u] = r.pos[p];
     }
+    // One run across the wave's batch: the run ids of its lowest position (the lanes' previous
+    // round) and its highest agree (wave-uniform LDS reads): no per-record run id or flush test.
+    bool one_run = false;
+#ifndef SCT_KEY_FASTPATH
+#define SCT_KEY_FASTPATH 1
+#endif
+    if (SCT_KEY_FASTPATH && tile_n == kKTile) {  // block-uniform
+      const int wo = t & ~(kWave - 1) & (kBlock - 1);
+      const int lo = (j0 == 0 ? 0 : (j0 - 1) * kBlock) + wo;
+      const int hi = (j0 + kKeyBatch - 1) * kBlock + wo + kWave - 1;
+      const int elo = __builtin_amdgcn_readfirstlane((int)s_e16[epad(lo)]);
+      const int ehi = __builtin_amdgcn_readfirstlane((int)s_e16[epad(hi)]);
+      one_run = elo == ehi;
+      if (one_run) cur_e = ebase + elo;
+    }
 #pragma unroll
     for (int u = 0; u < kKeyBatch; u++) {
       const int q = (j0 + u) * kBlock + t;
       const bool valid = q < tile_n;
       const int64_t p = base + q;
-      const int64_t e = valid ? ebase + (int64_t)s_e16[epad(q)] : cur_e;
-      wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
-      if (!valid) continue;
-      cur_e = e;
+      int64_t e = cur_e;
+      if (!one_run) {
+        e = valid ? ebase + (int64_t)s_e16[epad(q)] : cur_e;
+        wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
+        if (!valid) continue;
+        cur_e = e;
+      }
       uint32_t k1 = (uint32_t)vk1[u];
       uint32_t k2 = (uint32_t)vk2[u];
       if (k1 >= c.n_k1 || k2 >= c.n_k2) {  // invalid input: reported, never used as an index
