@@ -314,6 +314,22 @@ __device__ __forceinline__ uint64_t spread_bytes(uint32_t x) {
   return (v | (v << 7)) & 0x0101010101010101ull;
 }
 
+// The uy stream's exact-lane increments for one denominator (barcode lengths are fixed in a
+// chemistry): entry a holds fx_increments(RN(a / B)), computed as the other samples are, so a
+// table hit adds the same 8 words the arithmetic would.
+constexpr int kUyTab = 32;
+constexpr uint32_t kNoUyTab = 0xffffffffu;
+__device__ __forceinline__ void fill_uy_tab(uint32_t B, uint4* tab) {
+  const uint32_t a = threadIdx.x;
+  if (a >= (uint32_t)kUyTab) return;
+  const double x = (B != 0 && a <= B) ? ratio_y(a, B, 1.0 / (double)B) : 0.0;  // = ratio_rcp(a, B)
+  uint32_t inc[kStreamLanes - 1];
+  uint64_t inc7;
+  fx_increments(x, inc, inc7);
+  tab[2 * a] = make_uint4(inc[0], inc[1], inc[2], inc[3]);
+  tab[2 * a + 1] = make_uint4(inc[4], inc[5], inc[6], (uint32_t)inc7);
+}
+
 // A thread's open run of one gene.  The 16 counted flag bits are counted in bytes of pk (a run
 // stays open over the sub-tiles of one work item: at most kGeneChunk / kSub * kItems payloads),
 // two 64-bit adds per payload instead of one extract-and-add per flag.
@@ -327,11 +343,19 @@ struct GeneAcc {
 #pragma unroll
     for (int i = 0; i < 3 * kStreamLanes; i++) l[i] = 0;
   }
-  __device__ __forceinline__ void add(const GeneItem& g, const double* s_rcp) {
+  // uy_tab: the uy lane increments of a = 0 .. kUyTab - 1 over the work item's uy denominator uy_b
+  // (kNoUyTab: none); other denominators are computed
+  __device__ __forceinline__ void add(const GeneItem& g, const double* s_rcp, const uint4* uy_tab, uint32_t uy_b) {
     n += 1;
     pk[0] += spread_bytes(g.f & 0xffu);
     pk[1] += spread_bytes(g.f >> 8);
-    fx_accumulate(l + 0 * kStreamLanes, ratio_rcp(g.ua, g.ub, s_rcp));
+    if (g.ub == uy_b && g.ua <= uy_b) {
+      const uint4 i0 = uy_tab[2 * g.ua], i1 = uy_tab[2 * g.ua + 1];
+      l[0] += i0.x, l[1] += i0.y, l[2] += i0.z, l[3] += i0.w;
+      l[4] += i1.x, l[5] += i1.y, l[6] += i1.z, l[7] += i1.w;
+    } else {
+      fx_accumulate(l + 0 * kStreamLanes, ratio_rcp(g.ua, g.ub, s_rcp));
+    }
     const double yq = rcp_of(g.qb, s_rcp);  // the two gq quotients share the reciprocal
     fx_accumulate(l + 1 * kStreamLanes, ratio_y(g.qa, g.qb, yq));
     fx_accumulate(l + 2 * kStreamLanes, ratio_y(g.qs, g.qb, yq));
@@ -437,7 +461,7 @@ template <bool k8>
 __device__ __forceinline__ void gene_reduce_item(const void* __restrict__ pay, int64_t beg, int64_t end, uint32_t g0,
                                                  uint4* s_buf, int32_t* s_cbin, unsigned long long* s_lbin,
                                                  uint32_t* s_cnt, uint32_t* s_start, uint64_t* s_scan,
-                                                 const double* s_rcp) {
+                                                 const double* s_rcp, uint4* s_uytab) {
   using F = GeneFmt<k8>;
   using W = typename F::W;
   constexpr int kSub = F::kSub, kItems = kSub / kBlock;
@@ -445,6 +469,13 @@ __device__ __forceinline__ void gene_reduce_item(const void* __restrict__ pay, i
   const W* src = reinterpret_cast<const W*>(pay);
   W* s_sorted = reinterpret_cast<W*>(s_buf);
   const int t = threadIdx.x;
+#ifndef SCT_GENE_UYTAB
+#define SCT_GENE_UYTAB 1
+#endif
+  // the work item's first payload's uy denominator (block-uniform), tabulated when < kUyTab
+  const uint32_t ub0 = F::item(src[beg], g0).ub;
+  const uint32_t uy_b = (SCT_GENE_UYTAB && ub0 < (uint32_t)kUyTab) ? ub0 : kNoUyTab;
+  if (uy_b != kNoUyTab) fill_uy_tab(uy_b, s_uytab);  // visible after the first sub-tile's barriers
   GeneAcc acc;
   acc.clear();
   int cur = -1;
@@ -502,7 +533,7 @@ __device__ __forceinline__ void gene_reduce_item(const void* __restrict__ pay, i
         acc.clear();
         cur = (int)g.lg;
       }
-      acc.add(g, s_rcp);
+      acc.add(g, s_rcp, s_uytab, uy_b);
     }
     __syncthreads();  // s_sorted / s_cnt are reused by the next sub-tile
   }
@@ -523,6 +554,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
   __shared__ uint32_t s_start[kGenesPerBucket];
   __shared__ uint64_t s_scan[kWaves + 1];
   __shared__ double s_rcp[kRcpN];
+  __shared__ uint4 s_uytab[2 * kUyTab];
   if ((int64_t)blockIdx.x >= *n_work) return;  // block-uniform
   const int t = threadIdx.x;
   fill_rcp(s_rcp);  // visible after the first sub-tile's barriers
@@ -533,9 +565,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
   for (int i = t; i < kGenesPerBucket * kGeneCntPad; i += kBlock) s_cbin[i] = 0;
   for (int i = t; i < kGenesPerBucket * 3 * kStreamLanes; i += kBlock) s_lbin[i] = 0ull;
   if (*gwide)  // block-uniform
-    gene_reduce_item<false>(pay, beg, end, g0, s_buf, s_cbin, s_lbin, s_cnt, s_start, s_scan, s_rcp);
+    gene_reduce_item<false>(pay, beg, end, g0, s_buf, s_cbin, s_lbin, s_cnt, s_start, s_scan, s_rcp, s_uytab);
   else
-    gene_reduce_item<true>(pay, beg, end, g0, s_buf, s_cbin, s_lbin, s_cnt, s_start, s_scan, s_rcp);
+    gene_reduce_item<true>(pay, beg, end, g0, s_buf, s_cbin, s_lbin, s_cnt, s_start, s_scan, s_rcp, s_uytab);
   __syncthreads();
   // bins -> partial rows: counter lanes 0..14 are partial slots 0..14; stream lanes follow P_FLOAT
   for (int i = t; i < kGenesPerBucket * kGeneCnt; i += kBlock) {
