@@ -85,9 +85,14 @@ enum : uint16_t {
 struct Seg {
   uint32_t start, cnt, ent, flags;
 };
-struct Work {
-  uint32_t seg, chunk;
+struct alignas(16) Work {  // one chunk of a segment: its records [beg, beg + n), n <= kChunk
+  uint32_t seg, beg, n, pad;
 };
+__device__ __forceinline__ Work make_work(uint32_t id, uint32_t start, uint32_t cnt, uint32_t k) {
+  const uint32_t b = start + k * (uint32_t)kChunk;
+  const uint32_t r = start + cnt - b;
+  return Work{id, b, r < (uint32_t)kChunk ? r : (uint32_t)kChunk, 0u};
+}
 struct BucketCtl {  // device counters of one level (n_giant, n_big accumulate over levels)
   uint32_t n_seg, n_work, n_giant, err;  // err: a mapped ref id >= 2^kRefBits (set by build_keys)
   uint32_t n_big;
@@ -108,7 +113,7 @@ __device__ __forceinline__ void push_segment(const Seg& sg, Seg* __restrict__ se
   seg[id] = sg;
   const uint32_t nw = (sg.cnt + kChunk - 1) / kChunk;
   const uint32_t w0 = atomicAdd(&ctl->n_work, nw);
-  for (uint32_t k = 0; k < nw; k++) work[w0 + k] = Work{id, k};
+  for (uint32_t k = 0; k < nw; k++) work[w0 + k] = make_work(id, sg.start, sg.cnt, k);
 }
 
 // level 0: small entities are terminal buckets, mid-sized ones big buckets; larger ones segments
@@ -138,10 +143,9 @@ __global__ void __launch_bounds__(kBlock) k_bucket_hist(const uint64_t* __restri
   __shared__ uint32_t h[kWaves][kRadix];
   const int wid = threadIdx.x / kWave;
   for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&h[0][0])[i] = 0;
-  const Work wk = work[xcd_tile(blockIdx.x, gridDim.x)];
-  const Seg sg = seg[wk.seg];
-  const uint32_t beg = sg.start + wk.chunk * (uint32_t)kChunk;
-  const uint32_t end = (sg.start + sg.cnt - beg) < (uint32_t)kChunk ? sg.start + sg.cnt : beg + kChunk;
+  const Work wk = work[xcd_tile(blockIdx.x, gridDim.x)];  // the chunk's range rides in the work item:
+  const uint32_t beg = wk.beg;                             // no dependent segment load before the keys
+  const uint32_t end = wk.beg + wk.n;
   const uint64_t mask = (1ull << bits) - 1;
   __syncthreads();
   for (uint32_t p = beg + threadIdx.x; p < end; p += kBlock) atomicAdd(&h[wid][(keys[p] >> shift) & mask], 1u);
@@ -210,9 +214,8 @@ __global__ void __launch_bounds__(kBlock) k_bucket_scatter(const uint64_t* __res
   __shared__ uint64_t s_scan[kWaves + 1];
   const int t = threadIdx.x;
   const Work wk = work[xcd_tile(blockIdx.x, gridDim.x)];
-  const Seg sg = seg[wk.seg];
-  const uint32_t beg = sg.start + wk.chunk * (uint32_t)kChunk;
-  const int tile_n = (int)((sg.start + sg.cnt - beg) < (uint32_t)kChunk ? (sg.start + sg.cnt - beg) : kChunk);
+  const uint32_t beg = wk.beg;
+  const int tile_n = (int)wk.n;
   const uint32_t mask = (1u << bits) - 1;
   s_cnt[t] = 0;
   __syncthreads();
@@ -344,7 +347,7 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
   if (push) {
     const uint32_t id = s_base[0] + so;
     nseg[id] = Seg{start, c, sg.ent, fl};
-    for (uint32_t k = 0; k < nw; k++) nwork[s_base[1] + wo + k] = Work{id, k};
+    for (uint32_t k = 0; k < nw; k++) nwork[s_base[1] + wo + k] = make_work(id, start, c, k);
   }
 }
 
