@@ -39,8 +39,8 @@ ALG_BYTES = {
     "bucket_hist": 8,        # read w0
     "build_keys": 48,        # read cell/gene/umi/ref/pos (20) + bits/xf (2) + uy/gq/cy (10), write payload (16)
     "big_bucket": 18,        # read payload w0 + w1 (16) of the big buckets' records, write dflags (2)
-    "gene_emit": 32,         # read gene/bits/xf/dflags/uy/gq (16), write 16-byte gene payload
-    "gene_reduce": 16,       # read the 16-byte gene payload
+    "gene_emit": 24,         # read gene/bits/xf/dflags/uy/gq (16), write the 8-byte gene payload (16 when wide)
+    "gene_reduce": 8,        # read the 8-byte gene payload (16 when wide)
     "tag_row_scatter": 68,   # config 5, per pass: read a 32-byte row (SoA or packed), write it (+ 4-byte key)
     "tag_row_hist": 4,       # config 5, per pass: read the cell key
     "tag_pack": 64,          # tag sort with a tiebreak: read the 32-byte SoA record, write it packed
