@@ -7,7 +7,7 @@
 //   k_gene_plan    bucket starts from the per-bucket record counts (build_keys) -> the
 //                  emit cursors and the reduce work list;
 //   k_gene_emit    input order, coalesced: one payload per record into its gene bucket
-//                  (kGenesPerBucket genes), one cursor atomic per (block, bucket); 8 bytes
+//                  (kGenesPerBucket genes), at the range build_keys reserved per (tile, bucket); 8 bytes
 //                  (gene_payload8) when the stream operands fit, else 16 (GenePayload);
 //   k_gene_reduce  each block counting-sorts sub-tiles of one bucket's payloads by gene in
 //                  LDS, sums each thread's runs of equal gene in registers, adds runs into
@@ -110,52 +110,32 @@ struct EmitIn {
   }
 };
 
-// One block per kEmitTile records (input order, coalesced).  (1) count the block's records per
-// gene bucket (LDS atomics); (2) reserve one range per present bucket with one atomic on the
-// bucket's cursor (k_gene_plan set it to the bucket's start); (3) re-read the columns, rank
-// each record again within its bucket (a second LDS atomic: any order inside a range is fine,
-// the reduction is order-free) and write its payload at range + rank.  No per-record rank is
-// stored, so the tile can be large: a block's run per bucket is long and its payload stores
-// leave few partly written lines behind.  Each lane takes kEmitVec consecutive records per
-// round, so every column is read with one 4- to 16-byte load per lane (a wave covers 256
-// consecutive records per load); same-bucket lanes of one store get consecutive ranks (LDS
+// One block per key-pass tile (kEmitTile = build_keys' kKTile records, input order, coalesced).
+// build_keys counted the tile's records per gene bucket and reserved the tile's range in each
+// bucket with one atomic (gtoff[tile][bucket]: the range's offset inside the bucket), so a single
+// pass ranks each record within its bucket (an LDS atomic: any order inside a range is fine, the
+// reduction is order-free) and writes its payload at bucket start + offset + rank; the gene column
+// is read once.  Each lane takes kEmitVec consecutive records per round, so every column is read
+// with one 4- to 16-byte load per lane; same-bucket lanes of one store get consecutive ranks (LDS
 // atomics on one address return in lane order), so the stores coalesce.
-constexpr int kEmitTile = 4 * kTile;
+constexpr int kEmitTile = 2 * kTile;
 constexpr int kEmitRounds = kEmitTile / (kBlock * kEmitVec);
-constexpr int kEmitBatch = 8;  // rounds whose gene loads are in flight together in pass 1
-static_assert(kEmitRounds % kEmitBatch == 0, "whole batches");
 
 template <bool kFull, bool k8>
 __device__ __forceinline__ void gene_emit_tile(const int32_t* __restrict__ gene, const RecCols& r,
                                                const uint16_t* __restrict__ dflags, int64_t n, int64_t base,
-                                               uint32_t* __restrict__ cursor, int n_buckets, void* __restrict__ pay,
-                                               uint32_t* s_cnt, uint32_t* s_off) {
+                                               const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ toff,
+                                               int n_buckets, void* __restrict__ pay, uint32_t* s_cnt,
+                                               uint32_t* s_off) {
   const int t = threadIdx.x;
-  for (int i = t; i < n_buckets; i += kBlock) s_cnt[i] = 0;
-  __syncthreads();
-  // (1) counts: a batch of rounds' gene vectors loaded together, then counted
-  for (int j0 = 0; j0 < kEmitRounds; j0 += kEmitBatch) {
-    int32_t g[kEmitBatch][kEmitVec];
-#pragma unroll
-    for (int b = 0; b < kEmitBatch; b++) load_vec<kFull>(gene, base + ((j0 + b) * kBlock + t) * kEmitVec, n, g[b]);
-#pragma unroll
-    for (int b = 0; b < kEmitBatch; b++) {
-      const int q0 = ((j0 + b) * kBlock + t) * kEmitVec;
-#pragma unroll
-      for (int k = 0; k < kEmitVec; k++)
-        if (kFull || base + q0 + k < n) atomicAdd(&s_cnt[(uint32_t)g[b][k] / kGenesPerBucket], 1u);
-    }
-  }
-  __syncthreads();
-  // (2) one range per present bucket; the counters restart for the ranks of pass 3
+  // (entries of buckets absent from the tile were never written: read, never used)
   for (int i = t; i < n_buckets; i += kBlock) {
-    const uint32_t c = s_cnt[i];
-    if (c) s_off[i] = atomicAdd(&cursor[i], c);
     s_cnt[i] = 0;
+    s_off[i] = bstart[i] + toff[i];
   }
   __syncthreads();
-  // (3) payloads, software-pipelined: round j + 1's column loads are issued before round j's
-  // stores (vmcnt counts stores too, so loads issued after them would wait for them)
+  // software-pipelined: round j + 1's column loads are issued before round j's stores (vmcnt
+  // counts stores too, so loads issued after them would wait for them)
   EmitIn cur;
   cur.load<kFull>(gene, r, dflags, base + t * kEmitVec, n);
 #pragma unroll 2
@@ -183,20 +163,23 @@ __device__ __forceinline__ void gene_emit_tile(const int32_t* __restrict__ gene,
   }
 }
 
+// bstart: the bucket starts (k_gene_plan); gtoff: build_keys' per-(tile, bucket) range offsets
 __global__ void __launch_bounds__(kBlock) k_gene_emit(const int32_t* __restrict__ gene, RecCols r,
                                                       const uint16_t* __restrict__ dflags, int64_t n,
-                                                      uint32_t* __restrict__ cursor, int n_buckets,
+                                                      const uint32_t* __restrict__ bstart,
+                                                      const uint32_t* __restrict__ gtoff, int n_buckets,
                                                       const uint32_t* __restrict__ gwide, void* __restrict__ pay) {
   uint32_t* s_cnt = sct_dyn_lds;              // n_buckets (dynamic LDS)
   uint32_t* s_off = sct_dyn_lds + n_buckets;  // n_buckets
   const int64_t base = (int64_t)blockIdx.x * kEmitTile;
+  const uint32_t* toff = gtoff + (size_t)blockIdx.x * n_buckets;
   const bool full = base + kEmitTile <= n, wide = *gwide != 0;  // block-uniform
   if (wide) {
-    if (full) gene_emit_tile<true, false>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off);
-    else gene_emit_tile<false, false>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off);
+    if (full) gene_emit_tile<true, false>(gene, r, dflags, n, base, bstart, toff, n_buckets, pay, s_cnt, s_off);
+    else gene_emit_tile<false, false>(gene, r, dflags, n, base, bstart, toff, n_buckets, pay, s_cnt, s_off);
   } else {
-    if (full) gene_emit_tile<true, true>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off);
-    else gene_emit_tile<false, true>(gene, r, dflags, n, base, cursor, n_buckets, pay, s_cnt, s_off);
+    if (full) gene_emit_tile<true, true>(gene, r, dflags, n, base, bstart, toff, n_buckets, pay, s_cnt, s_off);
+    else gene_emit_tile<false, true>(gene, r, dflags, n, base, bstart, toff, n_buckets, pay, s_cnt, s_off);
   }
 }
 

@@ -44,7 +44,7 @@ namespace {
 
 struct Layout {
   size_t tile_cnt, scalars, scan_sums, keys_a, keys_b, vals_a, vals_b, counts, offsets, ent_start, partials;
-  size_t gcounts, gcursor, gwork, dflags, gpay, seen, zero_mito;
+  size_t gcounts, gcursor, gtoff, gwork, dflags, gpay, seen, zero_mito;
   size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, bigs, wctl, worder, total;
   int64_t num_tiles, num_chunks, max_ent, max_gene_work, max_seg, max_work;
   int n_buckets;
@@ -82,6 +82,7 @@ Layout layout_for(const sct_plan_t* plan) {
   L.partials = take(sizeof(int64_t) * SCT_NP * (size_t)L.max_ent);
   L.gcounts = take(L.gene ? sizeof(uint32_t) * (size_t)L.n_buckets : 0);  // records per gene bucket
   L.gcursor = take(L.gene ? sizeof(uint32_t) * (size_t)L.n_buckets : 0);
+  L.gtoff = take(L.gene ? sizeof(uint32_t) * (size_t)L.n_buckets * (size_t)cdiv(n1, kEmitTile) : 0);
   L.gwork = take(L.gene ? sizeof(int64_t) * 3 * (size_t)L.max_gene_work : 0);
   L.dflags = take(L.gene ? sizeof(uint16_t) * (size_t)n1 : 0);
   L.gpay = take(L.gene ? sizeof(GenePayload) * (size_t)n1 : 0);
@@ -293,17 +294,17 @@ template <bool kBucket, bool kStreams>
 int launch_build_keys(bool cell, bool gene, dim3 grid, hipStream_t s, const KeyCols& kc, const RecCols& rc2,
                       const uint8_t* mito, int64_t n, const uint64_t* toff, const Bits& b, uint64_t* keys,
                       void* vals, int64_t* ent_start, int64_t* partials, uint32_t* gcounts, int n_buckets,
-                      uint32_t* err, uint32_t* gwide) {
+                      uint32_t* err, uint32_t* gwide, uint32_t* gtoff) {
   if (cell && gene) {
     LAUNCH_SHM("build_keys", (k_build_keys_run<true, true, kBucket, kStreams>), grid, dim3(kBlock),
                sizeof(uint32_t) * (size_t)n_buckets, s, kc, rc2, mito, n, toff, b, keys, vals, ent_start, partials,
-               gcounts, n_buckets, err, gwide);
+               gcounts, n_buckets, err, gwide, gtoff);
   } else if (cell) {
     LAUNCH("build_keys", (k_build_keys_run<true, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito, n,
-           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide);
+           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide, gtoff);
   } else {
     LAUNCH("build_keys", (k_build_keys_run<false, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito,
-           n, toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide);
+           n, toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide, gtoff);
   }
   return SCT_OK;
 }
@@ -368,6 +369,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   int64_t* ent_start = at<int64_t>(ws, L.ent_start);
   int64_t* partials = at<int64_t>(ws, L.partials);
   uint32_t* gcounts = gene ? at<uint32_t>(ws, L.gcounts) : nullptr;
+  uint32_t* gtoff = gene ? at<uint32_t>(ws, L.gtoff) : nullptr;
   const uint8_t* mito = gene_is_mito;
   if (cell && !mito) {
     uint8_t* z = at<uint8_t>(ws, L.zero_mito);
@@ -391,14 +393,14 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   if (bucket) {
     uint64_t* va = at<uint64_t>(ws, L.vals_a);
     rc = streams ? launch_build_keys<true, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
-                                                 partials, gcounts, L.n_buckets, &ctl->err, gwide)
+                                                 partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff)
                  : launch_build_keys<true, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
-                                                  partials, gcounts, L.n_buckets, &ctl->err, gwide);
+                                                  partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff);
   } else {
     rc = streams ? launch_build_keys<false, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
-                                                  ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide)
+                                                  ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff)
                  : launch_build_keys<false, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
-                                                   ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide);
+                                                   ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff);
     if (rc) return rc;
     uint32_t err = 0;  // the bucket path reads the flag at its first level sync
     if (int rb = readback(&err, &ctl->err, sizeof(err), s)) return rb;
@@ -468,9 +470,10 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     void* gpay = at<GenePayload>(ws, L.gpay);
     LAUNCH_SHM("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), 2 * sizeof(uint32_t) * (size_t)(L.n_buckets + 1), s,
                (const uint32_t*)gcounts, L.n_buckets, gcur, gwork, n_gwork);
+    static_assert(kEmitTile == kKTile, "gene_emit tiles are the key pass's tiles (gtoff)");
     LAUNCH_SHM("gene_emit", k_gene_emit, dim3((unsigned)cdiv(n, kEmitTile)), dim3(kBlock),
-               2 * sizeof(uint32_t) * (size_t)L.n_buckets, s, rec->gene, rc2, (const uint16_t*)dflags, n, gcur,
-               L.n_buckets, (const uint32_t*)gwide, gpay);
+               2 * sizeof(uint32_t) * (size_t)L.n_buckets, s, rec->gene, rc2, (const uint16_t*)dflags, n,
+               (const uint32_t*)gcur, (const uint32_t*)gtoff, L.n_buckets, (const uint32_t*)gwide, gpay);
     HIPCHK(hipMemsetAsync(gene_partials, 0, sizeof(int64_t) * SCT_NP * (size_t)plan->n_gene_ids, s));
     LAUNCH("gene_reduce", k_gene_reduce, dim3((unsigned)L.max_gene_work), dim3(kBlock), s, (const void*)gpay,
            (const int64_t*)gwork, (const int64_t*)n_gwork, plan->n_gene_ids, (const uint32_t*)gwide, gene_partials);

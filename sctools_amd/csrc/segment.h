@@ -377,7 +377,8 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
                                                            int64_t* __restrict__ ent_start,
                                                            int64_t* __restrict__ partials,
                                                            uint32_t* __restrict__ gene_counts, int n_buckets,
-                                                           uint32_t* __restrict__ err, uint32_t* __restrict__ gwide) {
+                                                           uint32_t* __restrict__ err, uint32_t* __restrict__ gwide,
+                                                           uint32_t* __restrict__ gtoff) {
   static_assert(!kGene || kCell, "gene buckets come from the cell view");
   __shared__ uint16_t s_e16[kTilePad];
   __shared__ uint64_t s_scan[kWaves + 1];
@@ -499,8 +500,9 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
   wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
   if (kGene) {
     __syncthreads();
+    // the tile's range in each present bucket: its offset inside the bucket (k_gene_emit)
     for (int i = t; i < n_buckets; i += kBlock)
-      if (s_hist[i]) atomicAdd(&gene_counts[i], s_hist[i]);
+      if (s_hist[i]) gtoff[(size_t)blockIdx.x * n_buckets + i] = atomicAdd(&gene_counts[i], s_hist[i]);
   }
   if constexpr (kStreams) stream_tile<kCell>(r, base, tile_n, my_heads, my_ex, ebase, s_rcp, s_tab, partials,
                                                  kGene ? gwide : nullptr);
