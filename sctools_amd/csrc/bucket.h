@@ -299,7 +299,7 @@ __device__ __forceinline__ uint32_t split_flags(int Kb, int depth, int depth1, i
 __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restrict__ seg,
                                                             const uint32_t* __restrict__ hist,
                                                             uint32_t* __restrict__ cur, int depth, int bits,
-                                                            int K1, int KM, int KB, int parity,
+                                                            int K1, int KM, int KB, int parity, int by_ent,
                                                             uint16_t* __restrict__ bdesc, uint32_t* __restrict__ bent,
                                                             Seg* __restrict__ nseg, Work* __restrict__ nwork,
                                                             Seg* __restrict__ giants, Seg* __restrict__ bigs,
@@ -310,7 +310,7 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
   const int d = threadIdx.x;
   const size_t i = (size_t)blockIdx.x * kRadix + d;
   const Seg sg = seg[blockIdx.x];
-  const uint32_t c = hist[i];
+  const uint32_t c = hist[by_ent ? (size_t)sg.ent * kRadix + d : i];  // level 1: the key pass's per-entity counts
   s_c[d] = c;
   uint64_t tot_c;
   const uint32_t start = sg.start + (uint32_t)block_exclusive_scan<uint64_t>((uint64_t)c, &tot_c, s_scan);

@@ -42,9 +42,11 @@ using namespace sct;
 
 namespace {
 
+constexpr int64_t kEntHistMax = 1 << 18;  // entities whose first-level histogram the key pass builds
+
 struct Layout {
   size_t tile_cnt, scalars, scan_sums, keys_a, keys_b, vals_a, vals_b, counts, offsets, ent_start, partials;
-  size_t gcounts, gcursor, gtoff, gwork, dflags, gpay, seen, zero_mito;
+  size_t gcounts, gcursor, gtoff, gwork, dflags, gpay, seen, zero_mito, ent_hist;
   size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, bigs, wctl, worder, total;
   int64_t num_tiles, num_chunks, max_ent, max_gene_work, max_seg, max_work;
   int n_buckets;
@@ -88,6 +90,8 @@ Layout layout_for(const sct_plan_t* plan) {
   L.gpay = take(L.gene ? sizeof(GenePayload) * (size_t)n1 : 0);
   L.seen = take(L.gene ? sizeof(uint32_t) * (size_t)(plan->n_cell_ids > 0 ? plan->n_cell_ids : 1) : 0);
   L.zero_mito = take(L.gene ? (size_t)(plan->n_gene_ids > 0 ? plan->n_gene_ids : 1) : 0);
+  // the key pass's first-level digit counts per entity (1 KB each; larger plans use k_bucket_hist)
+  L.ent_hist = take(L.max_ent <= kEntHistMax ? sizeof(uint32_t) * kRadix * (size_t)L.max_ent : 0);
   // bucket.h: segments have > kBCap records and are disjoint within a level (and giants overall)
   L.max_seg = n1 / (kBCap + 1) + 2;
   L.max_work = n1 / kChunk + L.max_seg + 2;
@@ -194,7 +198,7 @@ int launch_hash_tile(bool cell, bool gene, dim3 grid, hipStream_t s, const uint1
 // the caller then reruns on the global-sort path.
 int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const int64_t* ent_start,
                     const uint8_t* mito, const Bits& b, bool cell, bool gene, int64_t* partials, uint16_t* dflags,
-                    hipStream_t s) {
+                    const uint32_t* ehist, hipStream_t s) {
   if (n == 0) return SCT_OK;
   uint64_t* ka = at<uint64_t>(ws, L.keys_a);
   uint64_t* kb = at<uint64_t>(ws, L.keys_b);
@@ -231,13 +235,17 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     const uint64_t* vin = src ? vb : va;
     uint64_t* kout = src ? ka : kb;
     uint64_t* vout = src ? va : vb;
-    HIPCHK(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kRadix * (size_t)h.n_seg, s));
-    LAUNCH("bucket_hist", k_bucket_hist, dim3(h.n_work), dim3(kBlock), s, kin, (const Seg*)seg[c],
-           (const Work*)work[c], shift, bits, hist);
+    // level 1's segments are entities: the key pass counted their digits (ehist)
+    const bool by_ent = level == 1 && ehist != nullptr;
+    if (!by_ent) {
+      HIPCHK(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kRadix * (size_t)h.n_seg, s));
+      LAUNCH("bucket_hist", k_bucket_hist, dim3(h.n_work), dim3(kBlock), s, kin, (const Seg*)seg[c],
+             (const Work*)work[c], shift, bits, hist);
+    }
     HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), s));  // next level's n_seg, n_work
     LAUNCH("bucket_classify", k_bucket_classify, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c],
-           (const uint32_t*)hist, cur, depth, bits, b.k1, b.k1 + b.k2, KB, level & 1, bdesc, bent, seg[c ^ 1],
-           work[c ^ 1], giants, bigs, ctl);
+           by_ent ? ehist : (const uint32_t*)hist, cur, depth, bits, b.k1, b.k1 + b.k2, KB, level & 1, by_ent ? 1 : 0,
+           bdesc, bent, seg[c ^ 1], work[c ^ 1], giants, bigs, ctl);
     // the next level's counts are final after classify: read them while the scatter runs
     if (int rb = readback_start(ctl, sizeof(h), s)) return rb;
     const uint32_t n_work = h.n_work;
@@ -294,17 +302,17 @@ template <bool kBucket, bool kStreams>
 int launch_build_keys(bool cell, bool gene, dim3 grid, hipStream_t s, const KeyCols& kc, const RecCols& rc2,
                       const uint8_t* mito, int64_t n, const uint64_t* toff, const Bits& b, uint64_t* keys,
                       void* vals, int64_t* ent_start, int64_t* partials, uint32_t* gcounts, int n_buckets,
-                      uint32_t* err, uint32_t* gwide, uint32_t* gtoff) {
+                      uint32_t* err, uint32_t* gwide, uint32_t* gtoff, uint32_t* ent_hist) {
   if (cell && gene) {
     LAUNCH_SHM("build_keys", (k_build_keys_run<true, true, kBucket, kStreams>), grid, dim3(kBlock),
                sizeof(uint32_t) * (size_t)n_buckets, s, kc, rc2, mito, n, toff, b, keys, vals, ent_start, partials,
-               gcounts, n_buckets, err, gwide, gtoff);
+               gcounts, n_buckets, err, gwide, gtoff, ent_hist);
   } else if (cell) {
     LAUNCH("build_keys", (k_build_keys_run<true, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito, n,
-           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide, gtoff);
+           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide, gtoff, ent_hist);
   } else {
     LAUNCH("build_keys", (k_build_keys_run<false, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito,
-           n, toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide, gtoff);
+           n, toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide, gtoff, ent_hist);
   }
   return SCT_OK;
 }
@@ -370,6 +378,9 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   int64_t* partials = at<int64_t>(ws, L.partials);
   uint32_t* gcounts = gene ? at<uint32_t>(ws, L.gcounts) : nullptr;
   uint32_t* gtoff = gene ? at<uint32_t>(ws, L.gtoff) : nullptr;
+  // bucket path: the key pass counts the first partition level's digits per entity
+  uint32_t* ehist = bucket && L.max_ent <= kEntHistMax && n_ent > 0 ? at<uint32_t>(ws, L.ent_hist) : nullptr;
+  if (ehist) HIPCHK(hipMemsetAsync(ehist, 0, sizeof(uint32_t) * kRadix * (size_t)n_ent, s));
   const uint8_t* mito = gene_is_mito;
   if (cell && !mito) {
     uint8_t* z = at<uint8_t>(ws, L.zero_mito);
@@ -393,14 +404,16 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   if (bucket) {
     uint64_t* va = at<uint64_t>(ws, L.vals_a);
     rc = streams ? launch_build_keys<true, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
-                                                 partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff)
+                                                 partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff, ehist)
                  : launch_build_keys<true, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
-                                                  partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff);
+                                                  partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff, ehist);
   } else {
     rc = streams ? launch_build_keys<false, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
-                                                  ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff)
+                                                  ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff,
+                                                  nullptr)
                  : launch_build_keys<false, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
-                                                   ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff);
+                                                   ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff,
+                                                   nullptr);
     if (rc) return rc;
     uint32_t err = 0;  // the bucket path reads the flag at its first level sync
     if (int rb = readback(&err, &ctl->err, sizeof(err), s)) return rb;
@@ -411,7 +424,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   // 2-3. distinct counts (+ per-record distinct events for the gene view)
   uint16_t* dflags = gene ? at<uint16_t>(ws, L.dflags) : nullptr;
   if (bucket) {
-    rc = bucket_distinct(L, ws, n, n_ent, ent_start, mito, b, cell, gene, partials, dflags, s);
+    rc = bucket_distinct(L, ws, n, n_ent, ent_start, mito, b, cell, gene, partials, dflags, ehist, s);
     if (rc == 1)  // a mapped ref id does not fit the bucket payload: redo on the global-sort path
       return pipeline(plan, rec, gene_is_mito, ws, ws_bytes, out_i, out_f, capacity, n_rows, gene_partials, s,
                       false);

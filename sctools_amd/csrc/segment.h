@@ -367,6 +367,7 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
 // global sort's (key with entity bits, u32 value with bit 31 = unmapped).
 // kStreams: also the exact quality-stream lanes of the runs (stream_tile), reusing the tile's
 // run ids: the stream ALU work overlaps the key pass's memory traffic in one launch.
+constexpr int kDhRuns = 4;  // runs of a tile whose first-level digit counts stay in LDS
 constexpr int kKeyBatch = 4;  // striped rounds whose column loads are issued together (8: occupancy 3, slower)
 static_assert(kKItems % kKeyBatch == 0, "whole batches");
 
@@ -378,7 +379,7 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
                                                            int64_t* __restrict__ partials,
                                                            uint32_t* __restrict__ gene_counts, int n_buckets,
                                                            uint32_t* __restrict__ err, uint32_t* __restrict__ gwide,
-                                                           uint32_t* __restrict__ gtoff) {
+                                                           uint32_t* __restrict__ gtoff, uint32_t* __restrict__ ent_hist) {
   static_assert(!kGene || kCell, "gene buckets come from the cell view");
   __shared__ uint16_t s_e16[kTilePad];
   __shared__ uint64_t s_scan[kWaves + 1];
@@ -396,6 +397,16 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
   if constexpr (kStreams) {  // visible after tile_run_ids' barriers
     fill_rcp(s_rcp);
     fill_stream_tabs<kCell>(r, base, s_tab);
+  }
+  // the first partition level's digit histogram per entity (bucket.h; ent_hist set on the bucket
+  // path): the tile's first kDhRuns runs count in LDS, later ones with global atomics
+  __shared__ uint32_t s_dh[kBucket ? kDhRuns * kRadix : 1];
+  const int KB = b.k1 + b.k2 + b.h;
+  const int bits1 = KB < kRadixBits ? KB : kRadixBits;
+  const int sh1 = KB - bits1;
+  if constexpr (kBucket) {
+    if (ent_hist)
+      for (int i = t; i < kDhRuns * kRadix; i += kBlock) s_dh[i] = 0;
   }
   // 1-2. run index of every record of the tile
   uint32_t my_heads, my_ex;
@@ -467,7 +478,14 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
       const uint32_t hsh = mapped ? frag_hash(ref, pos, rev ? 1u : 0u) : 0u;
       if constexpr (kBucket) {
         const bool mito = kCell ? k1_is_mito[k1] != 0 : false;
-        keys[p] = payload_w0(make_key(0, k1, k2, hsh, b), ref, rev, mapped, mito);
+        const uint64_t kp = make_key(0, k1, k2, hsh, b);
+        keys[p] = payload_w0(kp, ref, rev, mapped, mito);
+        if (ent_hist) {
+          const uint32_t dg = (uint32_t)(kp >> sh1) & ((1u << bits1) - 1u);
+          const int64_t loc = e - ebase;
+          if (loc < kDhRuns) atomicAdd(&s_dh[(int)loc * kRadix + dg], 1u);
+          else atomicAdd(&ent_hist[(size_t)e * kRadix + dg], 1u);
+        }
         static_cast<uint64_t*>(vals)[p] = ((uint64_t)p << 32) | (uint32_t)pos;
         if (mapped && (uint32_t)ref >= (1u << kRefBits)) atomicOr(err, 1u);
       } else {
@@ -498,6 +516,15 @@ __global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r,
     }
   }
   wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
+  if constexpr (kBucket) {
+    if (ent_hist) {
+      __syncthreads();
+      for (int i = t; i < kDhRuns * kRadix; i += kBlock) {
+        const uint32_t v = s_dh[i];
+        if (v) atomicAdd(&ent_hist[(size_t)(ebase + i / kRadix) * kRadix + (i % kRadix)], v);
+      }
+    }
+  }
   if (kGene) {
     __syncthreads();
     // the tile's range in each present bucket: its offset inside the bucket (k_gene_emit)
