@@ -41,7 +41,9 @@
 namespace sct {
 
 constexpr int kWin = 1024;                  // a tile owns the buckets starting in kWin positions
-constexpr int kBCap = kWin - 1;             // records of a terminal bucket
+constexpr int kHTCap = 2040;                // hash-tile table slots (not a power of two: the three
+                                            // tables fit 40 KB of LDS, 4 blocks per CU)
+constexpr int kBCap = kHTCap - kWin - 1;    // records of a terminal bucket (1015)
 constexpr int kTileCap = kWin + kBCap - 1;  // records per tile at most (2046)
 constexpr int kChunk = 2048;                // records per partition work item (LDS-staged)
 constexpr int kChunkItems = kChunk / kBlock;
@@ -65,6 +67,7 @@ constexpr int kBigBits = 12;
 constexpr int kBigSlots = 1 << kBigBits;
 constexpr int kBigCap = 3 * kBigSlots / 4 - 1;  // 3071
 static_assert(kTileCap < kHTSlots, "a tile's keys always fit its tables");
+static_assert(kTileCap < kHTCap, "a tile's keys always fit its tables");
 static_assert(kBigCap < kBigSlots && kBigSlots <= 4096, "big-bucket keys fit its tables; 12-bit slots");
 static_assert(kWin == 2 * kHBlock && (1 << kWinBits) == kWin, "window layout");
 static_assert(kBCap < (1 << 11), "count field");
@@ -379,6 +382,32 @@ __device__ __forceinline__ uint32_t ht_insert(E* T, E key, int& ev, int tb = kHT
   }
 }
 
+// ht_insert for a table of kHTCap slots: the home slot by multiply-shift range reduction of the
+// hashed key, probing with wrap-around at kHTCap.
+__device__ __forceinline__ uint32_t ht_home_cap(unsigned long long key) {
+  return (uint32_t)(((key * 0x9E3779B97F4A7C15ull) >> 32) * (unsigned long long)kHTCap >> 32);
+}
+__device__ __forceinline__ uint32_t ht_home_cap(unsigned int key) {
+  return (uint32_t)(((unsigned long long)(key * 0x9E3779B1u) * (unsigned long long)kHTCap) >> 32);
+}
+template <typename E>
+__device__ __forceinline__ uint32_t ht_insert_cap(E* T, E key, int& ev) {
+  uint32_t h = ht_home_cap(key);
+  while (true) {
+    const E old = atomicCAS(&T[h], (E)0, (E)(key | 1));
+    if (old == 0) {
+      ev = 1;
+      return h;
+    }
+    if ((old & ~(E)3) == key) {
+      ev = 0;
+      if (!(old & 2) && !(atomicOr(&T[h], (E)2) & 2)) ev = 2;
+      return h;
+    }
+    h = h + 1 == (uint32_t)kHTCap ? 0u : h + 1;
+  }
+}
+
 // kWideK1: k1 ids need more than kNarrowK1Bits bits (64-bit k1 table entries)
 template <bool kCell, bool kGene, bool kWideK1>
 __global__ void __launch_bounds__(kHBlock) k_hash_tile(const uint16_t* __restrict__ bdesc,
@@ -390,53 +419,68 @@ __global__ void __launch_bounds__(kHBlock) k_hash_tile(const uint16_t* __restric
                                                        int64_t* __restrict__ partials,
                                                        uint16_t* __restrict__ dflags) {
   using K1E = typename std::conditional<kWideK1, unsigned long long, unsigned int>::type;
-  __shared__ K1E s_k1[kHTSlots];                  // (bucket, k1)
-  __shared__ unsigned long long s_mol[kHTSlots];  // (bucket, k1, k2)
-  __shared__ unsigned long long s_frg[kHTSlots];  // (molecule slot, ref, strand, pos)
-  __shared__ uint16_t s_bd[kWin];                 // descriptor of the bucket starting at window offset x
-  __shared__ uint32_t s_bent[kWin];               // its entity
-  __shared__ uint32_t s_red[kHWaves];
-  __shared__ int s_last;
+  __shared__ K1E s_k1[kHTCap];                  // (bucket, k1)
+  __shared__ unsigned long long s_mol[kHTCap];  // (bucket, k1, k2)
+  __shared__ unsigned long long s_frg[kHTCap];  // (molecule slot, ref, strand, pos)
+  __shared__ uint64_t s_red[kHWaves];
+  __shared__ uint64_t s_lastp;
+  static_assert(kHTCap % 2 == 0 && (kHTCap * sizeof(K1E)) % 16 == 0, "tables cleared with 16-byte stores");
   const int t = threadIdx.x;
   const unsigned wb = xcd_tile(blockIdx.x, gridDim.x);
   const int64_t w0 = (int64_t)wb * kWin;
   const int win_n = (int)((n - w0) < kWin ? (n - w0) : kWin);
   // descriptors of window offsets 2t, 2t+1 and their entities (meaningful at bucket starts only,
-  // but loaded unconditionally so that no load waits for another: -0.09 ms per 100M records);
-  // tables cleared meanwhile
+  // but loaded unconditionally so that no load waits for another); tables cleared meanwhile
   const int p0 = 2 * t;
   uint16_t dsc[2];
   uint32_t ent[2];
 #pragma unroll
   for (int i = 0; i < 2; i++) {
-    dsc[i] = p0 + i < win_n ? bdesc[w0 + p0 + i] : (uint16_t)0;
-    ent[i] = p0 + i < win_n ? bent[w0 + p0 + i] : 0u;
+    const bool in = p0 + i < win_n;
+    dsc[i] = in ? bdesc[w0 + p0 + i] : (uint16_t)0;
+    ent[i] = in ? bent[w0 + p0 + i] : 0u;
   }
   {
     uint4* z = reinterpret_cast<uint4*>(s_mol);
-    for (int i = t; i < kHTSlots / 2; i += kHBlock) z[i] = make_uint4(0, 0, 0, 0);
+    for (int i = t; i < kHTCap / 2; i += kHBlock) z[i] = make_uint4(0, 0, 0, 0);
     z = reinterpret_cast<uint4*>(s_frg);
-    for (int i = t; i < kHTSlots / 2; i += kHBlock) z[i] = make_uint4(0, 0, 0, 0);
+    for (int i = t; i < kHTCap / 2; i += kHBlock) z[i] = make_uint4(0, 0, 0, 0);
     z = reinterpret_cast<uint4*>(s_k1);
-    for (int i = t; i < (int)(kHTSlots * sizeof(K1E) / 16); i += kHBlock) z[i] = make_uint4(0, 0, 0, 0);
+    for (int i = t; i < (int)(kHTCap * sizeof(K1E) / 16); i += kHBlock) z[i] = make_uint4(0, 0, 0, 0);
   }
-#pragma unroll
-  for (int i = 0; i < 2; i++) {
-    s_bd[p0 + i] = dsc[i];
-    s_bent[p0 + i] = ent[i];
+  // The bucket of window offset x is the last start at or before x: a max-scan of the packed
+  // (start + 1, descriptor, entity) of the starts carries the bucket's descriptor and entity to
+  // every position, so no LDS array of descriptors is needed.
+  const auto pack = [](int x, uint16_t d, uint32_t e) -> uint64_t {
+    return ((uint64_t)(x + 1) << 48) | ((uint64_t)d << 32) | e;
+  };
+  const uint64_t m0 = dsc[0] ? pack(p0, dsc[0], ent[0]) : 0ull;
+  const uint64_t m1 = dsc[1] ? pack(p0 + 1, dsc[1], ent[1]) : m0;
+  uint64_t ex;
+  {  // exclusive max-scan over the block (markers grow with the position: max = the latest start)
+    const int lane = t & (kWave - 1), wid = t / kWave;
+    uint64_t x = m1;
+    for (int off = 1; off < kWave; off <<= 1) {
+      const uint64_t y = __shfl_up(x, off);
+      if (lane >= off) x = y > x ? y : x;
+    }
+    if (lane == kWave - 1) s_red[wid] = x;
+    __syncthreads();
+    uint64_t carry = 0;
+    for (int w = 0; w < wid; w++) carry = s_red[w] > carry ? s_red[w] : carry;
+    uint64_t e1 = __shfl_up(x, 1);
+    if (lane == 0) e1 = 0;
+    ex = e1 > carry ? e1 : carry;
   }
-  // bucket of window offset x: the last start at or before x (max-scan of x + 1 markers)
-  const uint32_t m0 = dsc[0] ? (uint32_t)p0 + 1 : 0u;
-  const uint32_t m1 = dsc[1] ? (uint32_t)p0 + 2 : (m0);
-  const uint32_t ex = block_exclusive_max_n<kHBlock>(m1, s_red);  // has barriers
-  uint32_t inc[2];
+  uint64_t inc[2];
   inc[0] = m0 > ex ? m0 : ex;
   inc[1] = m1 > inc[0] ? m1 : inc[0];
-  if (t == kHBlock - 1) s_last = (int)inc[1] - 1;
+  if (t == kHBlock - 1) s_lastp = inc[1];
   __syncthreads();
-  const int last = s_last;
-  if (last < 0) return;  // block-uniform: no bucket starts in this window
-  const int end_off = last + (int)(s_bd[last] & BD_COUNT);  // the last bucket may run past the window
+  const uint64_t lastp = s_lastp;
+  if (lastp == 0) return;  // block-uniform: no bucket starts in this window
+  const int last = (int)(lastp >> 48) - 1;
+  const int end_off = last + (int)((lastp >> 32) & BD_COUNT);  // the last bucket may run past the window
 
   const int KB = b.k1 + b.k2 + b.h;
   const uint64_t kmask = (1ull << KB) - 1;
@@ -451,27 +495,28 @@ __global__ void __launch_bounds__(kHBlock) k_hash_tile(const uint16_t* __restric
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int q = (j < 2 ? 0 : kWin) + p0 + (j & 1);  // offset from w0
-    const int bs = j < 2 ? (int)inc[j] - 1 : last;    // the bucket's start offset = its ordinal
+    const uint64_t bp = j < 2 ? inc[j] : lastp;        // the bucket's (start + 1, descriptor, entity)
+    const int bs = (int)(bp >> 48) - 1;                 // the bucket's start offset = its ordinal
+    const uint32_t bd = (uint32_t)(bp >> 32) & 0xffffu;
     // inside the bucket's extent (a giant's range has no descriptor and follows some bucket)
-    const bool valid = j < 2 ? (bs >= 0 && q < win_n && q < bs + (int)(s_bd[bs] & BD_COUNT)) : (q < end_off);
-    const int64_t e = valid ? (int64_t)s_bent[bs] : cur_e;
+    const bool valid = j < 2 ? (bs >= 0 && q < win_n && q < bs + (int)(bd & BD_COUNT)) : (q < end_off);
+    const int64_t e = valid ? (int64_t)(uint32_t)bp : cur_e;
     wave_flush<kDistinct>(acc, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
     if (!valid) continue;
     cur_e = e;
-    const uint32_t bd = s_bd[bs];
     const bool pb = bd & BD_PARITY;
     const uint64_t x0 = pb ? w0_b[w0 + q] : w0_a[w0 + q];
     const uint64_t x1 = pb ? w1_b[w0 + q] : w1_a[w0 + q];
     const uint64_t key = (x0 >> kKeyShift) & kmask;  // ids >= the dictionary sizes stay inside KB bits
     int ek = 0, em, ef = 0;
     const uint32_t ms =
-        ht_insert<unsigned long long>(s_mol, (((uint64_t)bs << mol_bits) | (key >> sh_mol)) << 2, em);
+        ht_insert_cap<unsigned long long>(s_mol, (((uint64_t)bs << mol_bits) | (key >> sh_mol)) << 2, em);
     // A record whose molecule already had two records (em == 0) cannot change the (bucket, k1)
     // events: that group's inserter and first finder are among the molecule's first two records.
-    if (em != 0) ht_insert<K1E>(s_k1, (K1E)((((uint64_t)bs << b.k1) | (key >> sh_k1)) << 2), ek);
+    if (em != 0) ht_insert_cap<K1E>(s_k1, (K1E)((((uint64_t)bs << b.k1) | (key >> sh_k1)) << 2), ek);
     if (x0 & kW0Mapped) {
       const uint64_t fk = ((((uint64_t)ms << kFragBits) | payload_frag(x0)) << 32) | (uint32_t)x1;
-      ht_insert<unsigned long long>(s_frg, fk << 2, ef);
+      ht_insert_cap<unsigned long long>(s_frg, fk << 2, ef);
     }
     // split groups: only the first piece counts the head, and it also carries the multi event
     const bool k1_head = ek == 1 && !(bd & BD_K1_NOHEAD);
