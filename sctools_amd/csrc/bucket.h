@@ -553,8 +553,7 @@ __global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict_
   using K1E = typename std::conditional<kWideK1, unsigned long long, unsigned int>::type;
   __shared__ K1E s_k1[kBigSlots];
   __shared__ unsigned long long s_mol[kBigSlots];
-  __shared__ unsigned long long s_frg[kBigSlots];
-  __shared__ int32_t s_acc[kDistinct];
+  __shared__ unsigned long long s_frg[kBigSlots];  // 80 KB in all: 2 blocks per CU
   const int t = threadIdx.x;
   const Seg g = bigs[blockIdx.x];
   int tb = kHTBits;  // tables sized to the bucket: load factor <= 3/4
@@ -567,7 +566,6 @@ __global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict_
     for (int i = t; i < slots / 2; i += kBigBlock) z[i] = make_uint4(0, 0, 0, 0);
     z = reinterpret_cast<uint4*>(s_k1);
     for (int i = t; i < (int)(slots * sizeof(K1E) / 16); i += kBigBlock) z[i] = make_uint4(0, 0, 0, 0);
-    if (t < kDistinct) s_acc[t] = 0;
   }
   __syncthreads();
   const uint32_t bd = g.flags;
@@ -609,7 +607,8 @@ __global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict_
       dflags[x1 >> 32] = f;
     }
   }
-  // one entity per block: wave sums, then one LDS add per wave and lane, then the row
+  // one entity per block: wave sums, then one row atomic per wave and slot (no LDS, which keeps
+  // the block at 80 KB)
   const int lane = t & (kWave - 1);
   int32_t mine = 0;
 #pragma unroll
@@ -617,11 +616,9 @@ __global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict_
     const int32_t tot = wave_sum_dpp(acc[i]);
     mine = lane == i ? tot : mine;
   }
-  if (lane < kDistinct && mine) atomicAdd(&s_acc[lane], mine);
-  __syncthreads();
-  if (t < kDistinct && s_acc[t])
-    atomicAdd((unsigned long long*)&partials[(int64_t)g.ent * SCT_NP + distinct_slot(t)],
-              (unsigned long long)(int64_t)s_acc[t]);
+  if (lane < kDistinct && mine)
+    atomicAdd((unsigned long long*)&partials[(int64_t)g.ent * SCT_NP + distinct_slot(lane)],
+              (unsigned long long)(int64_t)mine);
 }
 
 // A bucket whose whole key' is fixed and still holds > kBCap records: one piece of one
