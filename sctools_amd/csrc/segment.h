@@ -302,16 +302,16 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
   const bool mine = t * kKItems < tile_n;
   int64_t lanes[kStreamLanes];
   int64_t cur_e = -1;
-  // the next (stream, half)'s columns are loaded before the current one is summed (software
-  // pipeline); a stream's lanes run over both halves and are flushed once
-  uint32_t wn[8], wd[8], nn[8], nd[8];
+  // a stream's lanes run over both halves and are flushed once.  (Loading the next half's columns
+  // before summing this one costs 16 VGPRs: the kernel then runs at 4 waves per SIMD instead of 5,
+  // 1.34 against 1.25 ms)
+  uint32_t wn[8], wd[8];
   uint32_t over = 0;  // operand bits above the narrow payload's fields (uy 5 bits, gq 9, gq_sum 15)
-  load(0, 0, wn, wd);
 #pragma unroll 1
   for (int sh = 0; sh < 2 * ns; sh++) {
     const int st = sh >> 1, h = sh & 1;
     const bool wide = (st == 1 || st == 2);
-    if (sh + 1 < 2 * ns) load((sh + 1) >> 1, (sh + 1) & 1, nn, nd);
+    load(st, h, wn, wd);
     if (h == 0) {
 #pragma unroll
       for (int i = 0; i < kStreamLanes; i++) lanes[i] = 0;
@@ -356,8 +356,6 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
       }
     }
     if (h == 1) wave_flush<kStreamLanes>(lanes, cur_e >= 0, cur_e, partials, slot);
-#pragma unroll
-    for (int k = 0; k < 8; k++) wn[k] = nn[k], wd[k] = nd[k];
   }
   if (gwide && __ballot(over != 0) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(gwide, 1u);
 }
@@ -372,7 +370,8 @@ constexpr int kKeyBatch = 4;  // striped rounds whose column loads are issued to
 static_assert(kKItems % kKeyBatch == 0, "whole batches");
 
 template <bool kCell, bool kGene, bool kBucket, bool kStreams>
-__global__ void __launch_bounds__(kBlock) k_build_keys_run(KeyCols c, RecCols r, const uint8_t* __restrict__ k1_is_mito,
+// 5 waves per SIMD (<= 96 VGPRs; 3 dwords spill, off the per-record loops)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) k_build_keys_run(KeyCols c, RecCols r, const uint8_t* __restrict__ k1_is_mito,
                                                            int64_t n, const uint64_t* __restrict__ tile_off, Bits b,
                                                            uint64_t* __restrict__ keys, void* __restrict__ vals,
                                                            int64_t* __restrict__ ent_start,
