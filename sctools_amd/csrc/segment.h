@@ -158,7 +158,7 @@ static_assert(kKTile <= 65535, "local run ids are 16-bit");
 __device__ __forceinline__ int64_t tile_run_ids(const int32_t* __restrict__ ent, int64_t base, int tile_n,
                                                 uint64_t tile_off, uint16_t* s_e16, uint64_t* s_hb,
                                                 uint64_t* s_scan, int64_t* __restrict__ ent_start,
-                                                uint32_t* my_heads, uint32_t* my_ex) {
+                                                uint32_t* my_heads, uint32_t* my_ex, uint32_t* n_heads) {
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
   for (int j0 = 0; j0 < kKItems; j0 += kRunBatch) {
     int32_t v[kRunBatch], pv[kRunBatch];
@@ -186,6 +186,7 @@ __device__ __forceinline__ int64_t tile_run_ids(const int32_t* __restrict__ ent,
   const int64_t ebase = (int64_t)tile_off - 1;
   *my_heads = heads;
   *my_ex = (uint32_t)ex;
+  *n_heads = (uint32_t)tot;  // the tile's last run has local id n_heads
   uint32_t loc = (uint32_t)ex;
   const int q0 = t * kKItems;
   uint32_t* s_w = reinterpret_cast<uint32_t*>(s_e16);
@@ -365,7 +366,7 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
 // global sort's (key with entity bits, u32 value with bit 31 = unmapped).
 // kStreams: also the exact quality-stream lanes of the runs (stream_tile), reusing the tile's
 // run ids: the stream ALU work overlaps the key pass's memory traffic in one launch.
-constexpr int kDhRuns = 4;  // runs of a tile whose first-level digit counts stay in LDS
+constexpr int kDhRuns = 5;  // LDS digit-count slots: the tile's first 4 runs and its last
 constexpr int kKeyBatch = 4;  // striped rounds whose column loads are issued together (8: occupancy 3, slower)
 static_assert(kKItems % kKeyBatch == 0, "whole batches");
 
@@ -408,9 +409,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
       for (int i = t; i < kDhRuns * kRadix; i += kBlock) s_dh[i] = 0;
   }
   // 1-2. run index of every record of the tile
-  uint32_t my_heads, my_ex;
+  uint32_t my_heads, my_ex, n_heads;
   const int64_t ebase = tile_run_ids(c.ent, base, tile_n, tile_off[(size_t)blockIdx.x * kKTilesPerBlock], s_e16,
-                                     s_hb, s_scan, ent_start, &my_heads, &my_ex);
+                                     s_hb, s_scan, ent_start, &my_heads, &my_ex, &n_heads);
+  // first-level digit counts: LDS slots for the tile's first kDhRuns - 1 runs and its last run
+  // (the runs that may continue into a neighbouring tile); runs wholly inside the tile (rarely
+  // segments) count with global atomics
+  const auto dh_slot = [n_heads](int64_t loc) -> int {
+    return loc < kDhRuns - 1 ? (int)loc : (loc == (int64_t)n_heads ? kDhRuns - 1 : -1);
+  };
 
   // 3. striped pass: keys, values and the run's additive metrics.  Runs are contiguous, so
   // in a round the wave's lanes cross a run boundary together: flush wave-cooperatively.
@@ -481,8 +488,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
         keys[p] = payload_w0(kp, ref, rev, mapped, mito);
         if (ent_hist) {
           const uint32_t dg = (uint32_t)(kp >> sh1) & ((1u << bits1) - 1u);
-          const int64_t loc = e - ebase;
-          if (loc < kDhRuns) atomicAdd(&s_dh[(int)loc * kRadix + dg], 1u);
+          const int sl = dh_slot(e - ebase);
+          if (sl >= 0) atomicAdd(&s_dh[sl * kRadix + dg], 1u);
           else atomicAdd(&ent_hist[(size_t)e * kRadix + dg], 1u);
         }
         static_cast<uint64_t*>(vals)[p] = ((uint64_t)p << 32) | (uint32_t)pos;
@@ -520,7 +527,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
       __syncthreads();
       for (int i = t; i < kDhRuns * kRadix; i += kBlock) {
         const uint32_t v = s_dh[i];
-        if (v) atomicAdd(&ent_hist[(size_t)(ebase + i / kRadix) * kRadix + (i % kRadix)], v);
+        const int sl = i / kRadix;
+        const int64_t loc = sl < kDhRuns - 1 ? sl : (int64_t)n_heads;  // slot kDhRuns - 1: the last run
+        if (v && (sl < kDhRuns - 1 || n_heads >= (uint32_t)(kDhRuns - 1)))
+          atomicAdd(&ent_hist[(size_t)(ebase + loc) * kRadix + (i % kRadix)], v);
       }
     }
   }
