@@ -204,52 +204,59 @@ __device__ __forceinline__ uint32_t digit_starts(uint32_t (*whist)[kRadix], uint
 // order inside a child bucket is irrelevant to the hash tiles), reserve one output range per
 // present digit with one atomic on the segment's cursor, and write each digit's records as a
 // contiguous run (LDS-staged, coalesced).  `shift` addresses w0 (key' bits + kKeyShift).
-__global__ void __launch_bounds__(kBlock) k_bucket_scatter(const uint64_t* __restrict__ kin,
-                                                           const uint64_t* __restrict__ vin,
-                                                           uint64_t* __restrict__ kout, uint64_t* __restrict__ vout,
-                                                           const Seg* __restrict__ seg, const Work* __restrict__ work,
-                                                           int shift, int bits, uint32_t* __restrict__ cur) {
+// kSBlock threads (4 records each): the 36 KB of staging allow 4 blocks per CU, so 512-thread
+// blocks keep twice the waves in flight of 256-thread ones.
+constexpr int kSBlock = 512;
+constexpr int kSItems = kChunk / kSBlock;
+static_assert(kRadix <= kSBlock, "one thread per digit");
+__global__ void __launch_bounds__(kSBlock) k_bucket_scatter(const uint64_t* __restrict__ kin,
+                                                            const uint64_t* __restrict__ vin,
+                                                            uint64_t* __restrict__ kout, uint64_t* __restrict__ vout,
+                                                            const Seg* __restrict__ seg, const Work* __restrict__ work,
+                                                            int shift, int bits, uint32_t* __restrict__ cur) {
   __shared__ uint64_t s_keys[kChunk];
   __shared__ uint64_t s_vals[kChunk];
   __shared__ uint32_t s_cnt[kRadix];
   __shared__ uint32_t s_start[kRadix];
   __shared__ uint32_t s_gbase[kRadix];
-  __shared__ uint64_t s_scan[kWaves + 1];
+  __shared__ uint64_t s_scan[kSBlock / kWave + 1];
   const int t = threadIdx.x;
   const Work wk = work[xcd_tile(blockIdx.x, gridDim.x)];
   const uint32_t beg = wk.beg;
   const int tile_n = (int)wk.n;
   const uint32_t mask = (1u << bits) - 1;
-  s_cnt[t] = 0;
+  if (t < kRadix) s_cnt[t] = 0;
   __syncthreads();
-  uint64_t k[kChunkItems];
-  uint64_t v[kChunkItems];
-  uint32_t rk[kChunkItems];
+  uint64_t k[kSItems];
+  uint64_t v[kSItems];
+  uint32_t rk[kSItems];
 #pragma unroll
-  for (int j = 0; j < kChunkItems; j++) {
-    const int q = j * kBlock + t;
+  for (int j = 0; j < kSItems; j++) {
+    const int q = j * kSBlock + t;
     if (q < tile_n) {
       k[j] = kin[beg + q];
       v[j] = vin[beg + q];
     }
   }
 #pragma unroll
-  for (int j = 0; j < kChunkItems; j++) {
-    const int q = j * kBlock + t;
+  for (int j = 0; j < kSItems; j++) {
+    const int q = j * kSBlock + t;
     if (q < tile_n) rk[j] = atomicAdd(&s_cnt[(uint32_t)(k[j] >> shift) & mask], 1u);
   }
   __syncthreads();
   {
-    const uint32_t c = s_cnt[t];
+    const uint32_t c = t < kRadix ? s_cnt[t] : 0u;
     uint64_t tot;
-    const uint32_t st = (uint32_t)block_exclusive_scan<uint64_t>((uint64_t)c, &tot, s_scan);
-    s_start[t] = st;
-    if (c) s_gbase[t] = atomicAdd(&cur[(size_t)wk.seg * kRadix + t], c);
+    const uint32_t st = (uint32_t)block_exclusive_scan_n<kSBlock, uint64_t>((uint64_t)c, &tot, s_scan);
+    if (t < kRadix) {
+      s_start[t] = st;
+      if (c) s_gbase[t] = atomicAdd(&cur[(size_t)wk.seg * kRadix + t], c);
+    }
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kChunkItems; j++) {
-    const int q = j * kBlock + t;
+  for (int j = 0; j < kSItems; j++) {
+    const int q = j * kSBlock + t;
     if (q < tile_n) {
       const uint32_t lp = s_start[(uint32_t)(k[j] >> shift) & mask] + rk[j];
       s_keys[lp] = k[j];
@@ -257,7 +264,7 @@ __global__ void __launch_bounds__(kBlock) k_bucket_scatter(const uint64_t* __res
     }
   }
   __syncthreads();
-  for (int q = t; q < tile_n; q += kBlock) {
+  for (int q = t; q < tile_n; q += kSBlock) {
     const uint64_t kk = s_keys[q];
     const uint32_t d = (uint32_t)(kk >> shift) & mask;
     const uint32_t o = s_gbase[d] + (uint32_t)(q - (int)s_start[d]);
@@ -339,9 +346,11 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
     bigs[atomicAdd(&ctl->n_big, 1u)] = Seg{start, c, sg.ent, fl | par};
   }
   const uint32_t nw = push ? (c + kChunk - 1) / kChunk : 0u;
-  uint64_t tot_s, tot_w;
-  const uint32_t so = (uint32_t)block_exclusive_scan<uint64_t>(push ? 1 : 0, &tot_s, s_scan);
-  const uint32_t wo = (uint32_t)block_exclusive_scan<uint64_t>(nw, &tot_w, s_scan);
+  // new segments and work items numbered by one scan of (segments << 32 | work items)
+  uint64_t tot_sw;
+  const uint64_t sw = block_exclusive_scan<uint64_t>(((uint64_t)(push ? 1 : 0) << 32) | nw, &tot_sw, s_scan);
+  const uint32_t so = (uint32_t)(sw >> 32), wo = (uint32_t)sw;
+  const uint64_t tot_s = tot_sw >> 32, tot_w = tot_sw & 0xffffffffull;
   if (d == 0 && tot_s) {
     s_base[0] = atomicAdd(&ctl->n_seg, (uint32_t)tot_s);
     s_base[1] = atomicAdd(&ctl->n_work, (uint32_t)tot_w);

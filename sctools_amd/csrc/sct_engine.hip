@@ -249,7 +249,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     // the next level's counts are final after classify: read them while the scatter runs
     if (int rb = readback_start(ctl, sizeof(h), s)) return rb;
     const uint32_t n_work = h.n_work;
-    LAUNCH("bucket_scatter", k_bucket_scatter, dim3(n_work), dim3(kBlock), s, kin, vin, kout, vout,
+    LAUNCH("bucket_scatter", k_bucket_scatter, dim3(n_work), dim3(kSBlock), s, kin, vin, kout, vout,
            (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
     if (int rb = readback_finish(&h, sizeof(h))) return rb;
     c ^= 1;
