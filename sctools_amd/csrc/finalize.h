@@ -7,15 +7,32 @@
 namespace sct {
 
 // MetricAggregator.finalize (aggregator.py:342-387), CellMetrics.finalize (463-490),
-// GeneMetrics.finalize (571-578): one thread per row.
+// GeneMetrics.finalize (571-578): kFinThreads threads per row -- thread 0 the integer columns and
+// ratios, thread s the exact mean / variance of stream s (each a few big-integer divisions, so a
+// row's four streams run side by side).  Launch with rows * kFinThreads threads.
+constexpr int kFinThreads = 4;
+static_assert(kFinThreads == kStreams, "one thread per quality stream");
 __global__ void k_finalize(const int64_t* __restrict__ partials, int64_t rows, int mode, int exact,
                            const int64_t* __restrict__ ent_start, int64_t* __restrict__ out_i,
                            double* __restrict__ out_f) {
-  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t idx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t r = idx / kFinThreads;
+  const int st = (int)(idx % kFinThreads);
   if (r >= rows) return;
   const int64_t* P = partials + r * SCT_NP;
   int64_t* I = out_i + r * SCT_NI;
   double* F = out_f + r * SCT_NF;
+  if (exact) {
+    const int mean_col = st == 0 ? SCT_F_UY_MEAN : st == 1 ? SCT_F_GQF_MEAN : st == 2 ? SCT_F_GQ_MEAN : SCT_F_CY_MEAN;
+    const int var_col = st == 0 ? SCT_F_UY_VAR : st == 1 ? SCT_F_GQF_VAR : st == 2 ? SCT_F_GQ_VAR : SCT_F_CY_VAR;
+    if (st < 3 || mode == SCT_MODE_CELL) {
+      fx_finalize(P + P_FLOAT + st * kStreamLanes, P[P_N_READS], &F[mean_col], &F[var_col]);
+    } else {
+      F[mean_col] = 0.0;
+      F[var_col] = 0.0;
+    }
+  }
+  if (st != 0) return;
   const int64_t n_reads = P[P_N_READS];
   const int64_t n_mol = P[P_N_MOL];
   const int64_t n_frag = P[P_N_FRAG];
@@ -50,17 +67,6 @@ __global__ void k_finalize(const int64_t* __restrict__ partials, int64_t rows, i
   F[SCT_F_FRAGMENTS_PER_MOLECULE] = n_mol ? (double)n_frag / (double)n_mol : qnan;
   const int64_t mito = P[P_MITO_READS];
   F[SCT_F_PCT_MITO] = mito ? ((double)mito / (double)n_reads) * 100.0 : 0.0;
-  if (exact) {
-    fx_finalize(P + P_FLOAT + 0 * kStreamLanes, n_reads, &F[SCT_F_UY_MEAN], &F[SCT_F_UY_VAR]);
-    fx_finalize(P + P_FLOAT + 1 * kStreamLanes, n_reads, &F[SCT_F_GQF_MEAN], &F[SCT_F_GQF_VAR]);
-    fx_finalize(P + P_FLOAT + 2 * kStreamLanes, n_reads, &F[SCT_F_GQ_MEAN], &F[SCT_F_GQ_VAR]);
-    if (mode == SCT_MODE_CELL) {
-      fx_finalize(P + P_FLOAT + 3 * kStreamLanes, n_reads, &F[SCT_F_CY_MEAN], &F[SCT_F_CY_VAR]);
-    } else {
-      F[SCT_F_CY_MEAN] = 0.0;
-      F[SCT_F_CY_VAR] = 0.0;
-    }
-  }
 }
 
 // OnlineGaussianSufficientStatistic.update (stats.py:82-87), one operation per rounding

@@ -449,7 +449,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   }
 
   if (out_i) {
-    LAUNCH("finalize", k_finalize, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, (const int64_t*)partials,
+    LAUNCH("finalize", k_finalize, dim3((unsigned)cdiv(n_ent * kFinThreads, kBlock)), dim3(kBlock), s, (const int64_t*)partials,
            n_ent, cell ? SCT_MODE_CELL : SCT_MODE_GENE, exact ? 1 : 0, (const int64_t*)ent_start, out_i, out_f);
     if (!exact) {  // sequential Welford: big entities one wave each (largest first), small ones a lane each
       const dim3 egrid((unsigned)cdiv(n_ent, kBlock));
@@ -1020,7 +1020,7 @@ int sct_finalize_partials(int32_t mode, const int64_t* partials, int64_t rows, i
     return fail(SCT_EINVAL, "bad finalize arguments");
   if (rows == 0) return SCT_OK;
   hipStream_t s = (hipStream_t)stream;
-  LAUNCH("finalize", k_finalize, dim3((unsigned)cdiv(rows, kBlock)), dim3(kBlock), s, partials, rows, (int)mode, 1,
+  LAUNCH("finalize", k_finalize, dim3((unsigned)cdiv(rows * kFinThreads, kBlock)), dim3(kBlock), s, partials, rows, (int)mode, 1,
          (const int64_t*)nullptr, out_ints, out_floats);
   return SCT_OK;
 }
