@@ -29,8 +29,21 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-PEAK_HBM = 8.0e12
-PROFILE_STEPS = 2  # untimed steps with every kernel timed (the per-kernel table)  # MI355X HBM3E spec, MI355X_MICROARCH.md
+PEAK_HBM = 8.0e12  # MI355X HBM3E spec, MI355X_MICROARCH.md
+PROFILE_STEPS = 2  # untimed steps with every kernel timed (the per-kernel table)
+
+# The unmodified reference Python gatherer timed in the build container (BASELINE.md "Measured CPU
+# reference"; it cannot run on the GPU box): context for `value`, not the cpu_baseline leg.
+REFERENCE_PYTHON = {
+    "value": 39038.0,
+    "unit": "records/s",
+    "cores": 1,
+    "kind": "reference (Python, unmodified)",
+    "host": "build container: Intel Xeon, 8 cores, 1 thread per core (not the GPU box)",
+    "sample": "GatherCellMetrics aggregation of 200k pre-decoded 10x-v2-shaped records, 20 cells, 30k genes; "
+              "stub pysam records, BAM decode excluded (BASELINE.md table, SURVEY.md 6)",
+    "value_8_processes": 268000.0,
+}
 
 # Algorithmic HBM bytes per record per launch of each kernel.
 ALG_BYTES = {
@@ -55,7 +68,7 @@ ALG_BYTES = {
 
 
 # HIP-event kernel names (engine profile) -> rocprofv3 kernel names (tools/pmc_traffic.py keys)
-PMC_NAMES = {"build_keys": "build_keys_run", "scan": "scan_wide"}
+PMC_NAMES = {"build_keys": "build_keys_run", "scan": "scan_wide", "heads": "heads4"}
 
 
 def pipeline_bytes(args, dims):
@@ -93,7 +106,7 @@ def parse():
                     help="config 5: the order sorted inside every step -- (CB, UB, GE) then query name, as "
                          "bam.sort_by_tags_and_queryname (bam.py:698-709) / TagSortBam define it (default), "
                          "or CB only (all the cell and grouped gene metrics need)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"),
                     help="rocprofv3 --pmc per-kernel HBM bytes (tools/pmc_passes.sh) for roofline.traffic")
     return ap.parse_args()
 
@@ -193,7 +206,7 @@ def main():
         step()
     torch.cuda.synchronize()
     eng.profile_enable(False)
-    table = eng.profile_read()
+    table = eng.profile_read_items()
     dom_name = max(table.items(), key=lambda kv: kv[1][0])[0] if table else ""
     if world > 1:
         dist.barrier()
@@ -209,8 +222,9 @@ def main():
         dist.barrier()
     eng.profile_enable(False)
     eng.profile_only("")
-    prof = eng.profile_read()
+    prof = eng.profile_read_items()
     elapsed = t1 - t0
+    allreduce_ms = time_allreduce(partials, dev) if world > 1 else None
     side = side_measurements(eng, data, dims, mito, multi, args, regroup) if rank == 0 else {}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -227,9 +241,12 @@ def main():
     value = total_records / elapsed
     # dominant kernel: largest total in the profiling pass; its average launch time comes from the HIP
     # events that bracketed only its launches in the timed region (on its launch stream)
-    dom_ms, dom_launches = prof.get(dom_name, (0.0, 1))
+    # (items: what its launches processed -- records, segment records, sort items -- as the engine
+    # reports them per launch; the records of the shard where a launch does not report them)
+    dom_ms, dom_launches, dom_items = prof.get(dom_name, (0.0, 1, -1))
     avg_s = dom_ms / 1e3 / max(1, dom_launches)
-    per_launch_bytes = ALG_BYTES.get(dom_name, 0) * args.records
+    items_per_launch = dom_items / max(1, dom_launches) if dom_items >= 0 else float(args.records)
+    per_launch_bytes = ALG_BYTES.get(dom_name, 0) * items_per_launch
     achieved = per_launch_bytes / avg_s if avg_s > 0 else 0.0
     roofline = {
         "bound": "hbm",
@@ -242,15 +259,24 @@ def main():
         "traffic_source": None,
         "avg_launch_ms": avg_s * 1e3,
         "launches_per_step": dom_launches / args.steps,
-        "alg_bytes_per_record": ALG_BYTES.get(dom_name, 0),
-        # whole pipeline against SURVEY.md 8(d)'s B_alg = 32 + 12 + 24*P + 44 bytes/record
-        "pipeline_alg_bytes_per_record": pipeline_bytes(args, dims),
-        "pipeline_frac": value / world * pipeline_bytes(args, dims) / PEAK_HBM,
+        "alg_bytes_per_item": ALG_BYTES.get(dom_name, 0),
+        "items_per_launch": items_per_launch,
+        "items_source": "engine (per launch)" if dom_items >= 0 else "records of the shard",
+        # SURVEY.md 8(d)'s model of a sort pipeline (B_alg = 32 + 12 + 24*P + 44 bytes/record, a
+        # 7-pass LSD sort this pipeline does not run): a yardstick, not this pipeline's traffic
+        "model_alg_bytes_per_record": pipeline_bytes(args, dims),
+        "model_frac": value / world * pipeline_bytes(args, dims) / PEAK_HBM,
     }
     traffic = pmc_traffic(args, dom_name)
     if traffic is not None:
         roofline["traffic"], roofline["traffic_source"] = traffic
+    # the whole step's measured HBM bytes: PMC bytes per launch x launches per step, every kernel
+    step_traffic = pmc_step_traffic(args, table)
+    if step_traffic is not None:
+        roofline["step_traffic_bytes"] = step_traffic
+        roofline["step_traffic_frac"] = step_traffic / (elapsed / args.steps) / PEAK_HBM
     kernel_ms_per_step = {k: round(v[0] / PROFILE_STEPS, 4) for k, v in sorted(table.items(), key=lambda kv: -kv[1][0])}
+    kernel_items_per_step = {k: (v[2] / PROFILE_STEPS if v[2] >= 0 else None) for k, v in table.items()}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -286,9 +312,12 @@ def main():
             },
             "roofline": roofline,
             "kernel_ms_per_step": kernel_ms_per_step,
+            "kernel_items_per_step": kernel_items_per_step,
             "kernel_table_source": "untimed profiling pass of %d steps (HIP events around every kernel)" % PROFILE_STEPS,
             "cpu_baseline": cpu,
             "speedup_vs_cpu_baseline": (value / cpu["value"]) if cpu else None,
+            "reference_python": REFERENCE_PYTHON,
+            "allreduce_ms": allreduce_ms,
         }
         out.update(side)
         if "h2d" in side:
@@ -343,10 +372,27 @@ def side_measurements(eng, data, dims, mito, multi, args, regroup):
     return out
 
 
-def pmc_traffic(args, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
-    (tools/pmc_passes.sh -> tools/pmc_traffic.py), if it was measured on this engine source and
-    this workload; else None (the roofline then reports traffic null)."""
+def time_allreduce(partials, dev, reps=20):
+    """The gene-partial all-reduce alone (RCCL over xGMI, [n_gene_ids, 64] int64), ms per call:
+    the collective's cost beside records/s (its result is discarded: partials are re-summed)."""
+    from sctools_amd import distributed as D
+
+    buf = partials.clone()
+    D.allreduce_partials(buf)
+    torch.cuda.synchronize()
+    dist.barrier()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        D.allreduce_partials(buf)
+    b.record()
+    torch.cuda.synchronize()
+    t = torch.tensor([a.elapsed_time(b) / reps], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _traffic_file(args):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from pmc_traffic import source_hash
 
@@ -354,10 +400,36 @@ def pmc_traffic(args, kernel):
     if not path or not os.path.exists(path) or args.records != 100_000_000 or args.cells != 10_000:
         return None
     d = json.load(open(path))
-    kernel = PMC_NAMES.get(kernel, kernel)
-    if d.get("source_sha256") != source_hash(ROOT) or kernel not in d.get("kernels", {}):
+    if d.get("source_sha256") != source_hash(ROOT):
         return None
-    return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return d
+
+
+def pmc_step_traffic(args, table):
+    """HBM bytes of one step: every engine kernel's PMC bytes per launch (the committed rocprofv3 --pmc
+    summary of this engine source) times its launches per step (the profiling pass); None if any
+    kernel of the step has no PMC figure."""
+    d = _traffic_file(args)
+    if d is None:
+        return None
+    tot = 0.0
+    for k, v in table.items():
+        pk = PMC_NAMES.get(k, k)
+        if pk not in d["kernels"]:
+            return None
+        tot += d["kernels"][pk]["hbm_bytes_per_launch"] * v[1] / PROFILE_STEPS
+    return tot
+
+
+def pmc_traffic(args, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
+    (tools/pmc_passes.sh -> tools/pmc_traffic.py), if it was measured on this engine source and
+    this workload; else None (the roofline then reports traffic null)."""
+    d = _traffic_file(args)
+    kernel = PMC_NAMES.get(kernel, kernel)
+    if d is None or kernel not in d.get("kernels", {}):
+        return None
+    return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(args.traffic_json, ROOT)
 
 
 def cpu_baseline(data, args):

@@ -31,6 +31,8 @@ extern "C" {
 #define SCT_BAM_VALUEERROR -13  /* invalid clipping, or a record beyond the 32-byte columnar limits */
 #define SCT_BAM_EMPTY -14       /* no records (RuntimeError: StopIteration in iter_tag_groups) */
 #define SCT_BAM_MISSING_TAG -15 /* sct_bam_split: a record carries none of the tags (RuntimeError, bam.py:286-289) */
+#define SCT_BAM_ETYPED -16      /* sct_bam_decode*: a dictionary tag holds a float or array value (or, for
+                                 * SCT_BAM_SORT_KEYS, an integer): decode with the Python reader instead */
 
 #define SCT_BAM_CELL_METRICS 0 /* require CY (and CR where CB is present), as CellMetrics does   */
 #define SCT_BAM_GENE_METRICS 1 /* records of multi-gene GE values are not validated (gatherer.py:210-212) */

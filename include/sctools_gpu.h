@@ -234,6 +234,11 @@ int sct_comm_unique_id(uint8_t* id, size_t bytes);
 int sct_comm_init_rank(void** comm, int nranks, const uint8_t* id, size_t bytes, int rank, int device);
 int sct_comm_init_all(void** comms, int ndev, const int* devices);
 int sct_comm_destroy(void* comm);
+/* Abort a communicator whose peers may never arrive (ncclCommAbort): a rank failed before
+ * or during the all-reduce.  Pending RCCL work on it is cancelled and the communicator is
+ * freed; it must not be used or destroyed afterwards.  (New plumbing: the reference merges
+ * CSV files and has no collective to abort.) */
+int sct_comm_abort(void* comm);
 
 /* ---- tag sort (TagSortBam / bam.sort_by_tags_and_queryname, bam.py:638-709;
  *      platform.py:55-104) ---- */
@@ -315,6 +320,10 @@ int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void*
 int sct_profile_enable(int on);
 int sct_profile_only(const char* kernel_name);
 int sct_profile_read(const char** names, double* ms, int64_t* launches, int max_kernels);
+/* sct_profile_read plus, per kernel, the items its timed launches processed in all (records,
+ * payloads or sort items: what the algorithmic bytes per item of the roofline multiply), or -1
+ * when a launch of that kernel does not report them. */
+int sct_profile_read_items(const char** names, double* ms, int64_t* launches, int64_t* items, int max_kernels);
 
 #ifdef __cplusplus
 }

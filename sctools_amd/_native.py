@@ -35,9 +35,10 @@ RECORD_COLUMNS = ("cell", "umi", "gene", "ref", "pos", "gq_sum", "gq_len", "gq_g
 EXPORTED = ("sct_abi_version", "sct_last_error", "sct_workspace_size", "sct_count_entities",
             "sct_compute_metrics", "sct_gene_partials", "sct_cell_metrics_gene_partials",
             "sct_finalize_partials", "sct_profile_enable", "sct_profile_only", "sct_profile_read",
+            "sct_profile_read_items",
             "sct_tag_sort_workspace_size", "sct_tag_sort", "sct_verify_sort", "sct_count_matrix_workspace_size", "sct_count_matrix",
             "sct_allreduce_gene_partials", "sct_comm_unique_id", "sct_comm_init_rank", "sct_comm_init_all",
-            "sct_comm_destroy")
+            "sct_comm_destroy", "sct_comm_abort")
 ORDER_CELL, ORDER_CELL_UMI_GENE, ORDER_GENE_CELL_UMI = 0, 1, 2
 PLAN_GENE_PARTIALS = 0x1
 
@@ -153,6 +154,8 @@ def load() -> ctypes.CDLL:
     L.sct_comm_init_all.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.sct_comm_destroy.restype = ctypes.c_int
     L.sct_comm_destroy.argtypes = [vp]
+    L.sct_comm_abort.restype = ctypes.c_int
+    L.sct_comm_abort.argtypes = [vp]
     L.sct_profile_enable.restype = ctypes.c_int
     L.sct_profile_enable.argtypes = [ctypes.c_int]
     L.sct_profile_only.restype = ctypes.c_int
@@ -160,6 +163,9 @@ def load() -> ctypes.CDLL:
     L.sct_profile_read.restype = ctypes.c_int
     L.sct_profile_read.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(i64), ctypes.c_int]
+    L.sct_profile_read_items.restype = ctypes.c_int
+    L.sct_profile_read_items.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
     if L.sct_abi_version() != SCT_ABI_VERSION:
         raise ImportError("libsctools_gpu.so ABI %d != %d" % (L.sct_abi_version(), SCT_ABI_VERSION))
     _lib = L

@@ -492,28 +492,50 @@ def verify_sort(records, tag_keys) -> None:
 
 
 def _sort_keys(path: str, tag_keys):
-    """(keys, key names, query-name ranks, query names) of a BAM: up to three tags as ranks of
-    their sorted string values (native decode, "" for a missing tag), more as ranks of the
-    value tuples (host); query names as ranks of the sorted names."""
-    import numpy as np
-
+    """(keys, key names, query-name ranks, query names) of a BAM: up to three string-valued tags as
+    ranks of their sorted values (native decode, "" for a missing tag); query names as ranks of the
+    sorted names.  More tags, or a tag holding integer / float / array values, go through
+    _typed_sort_keys: Python's own comparisons of the values (ints numerically; an int against a
+    str raises TypeError, as the reference's sorted() does)."""
     from sctools_amd import bamnative
 
     if len(tag_keys) <= 3:
         pad = [t for t in ("~0", "~1", "~2") if t not in tag_keys][: 3 - len(tag_keys)]
-        arrays, names = bamnative.decode(path, "sortkeys", tags=tuple(list(tag_keys) + pad))
+        try:
+            arrays, names = bamnative.decode(path, "sortkeys", tags=tuple(list(tag_keys) + pad))
+        except bamnative.TypedTagValue:
+            return _typed_sort_keys(path, tag_keys)
         keys = [arrays["cell"], arrays["umi"], arrays["gene"]][: len(tag_keys)]
         key_names = [["" if v is None else v for v in nm] for nm in names[: len(tag_keys)]]
-        return keys, key_names, arrays["qname"], names[3]
-    # more tags than the native key columns (rare: the reference CLIs pass three): tuples on the host
-    recs = [(tuple("" if v is None else str(v) for v in (get_tag_or_default(r, k, "") for k in tag_keys)),
-             r.query_name) for r in open_alignments(path, "rb")]
-    tuples = sorted(set(t for t, _ in recs))
-    trank = {t: i for i, t in enumerate(tuples)}
+        return keys, key_names, arrays["qname"], names[3], False
+    return _typed_sort_keys(path, tag_keys)
+
+
+def _ranks(values):
+    """(rank of each value, distinct values in order) under Python's comparisons -- unhashable
+    values (arrays) included; mixed incomparable types raise TypeError as sorted() does."""
+    order = sorted(range(len(values)), key=lambda i: values[i])
+    rank = [0] * len(values)
+    distinct = []
+    for i in order:
+        if not distinct or values[i] != distinct[-1]:
+            distinct.append(values[i])
+        rank[i] = len(distinct) - 1
+    return rank, distinct
+
+
+def _typed_sort_keys(path: str, tag_keys):
+    """_sort_keys on the host with the tags' Python values (get_tag_or_default(r, k, ""),
+    bam.py:655-656): the value tuples are ranked with Python's comparisons (one key column; the
+    last element True says so)."""
+    import numpy as np
+
+    recs = [(tuple(get_tag_or_default(r, k, "") for k in tag_keys), r.query_name) for r in open_alignments(path, "rb")]
+    trank, tuples = _ranks([t for t, _ in recs])
     qs = sorted(set(q for _, q in recs))
     qr = {q: i for i, q in enumerate(qs)}
-    return ([np.array([trank[t] for t, _ in recs], dtype=np.int32)], [[list(t) for t in tuples]],
-            np.array([qr[q] for _, q in recs], dtype=np.int32), qs)
+    return ([np.array(trank, dtype=np.int32)], [[list(t) for t in tuples]],
+            np.array([qr[q] for _, q in recs], dtype=np.int32), qs, True)
 
 
 def _key_columns(eng, keys, key_names, n):
@@ -542,9 +564,13 @@ def verify_bam_sort(path: str, tag_keys, device=None) -> None:
     from sctools_amd import engine as E
 
     tag_keys = list(tag_keys)
-    keys, key_names, qrank, qnames = _sort_keys(path, tag_keys)
+    keys, key_names, qrank, qnames, typed = _sort_keys(path, tag_keys)
     n = int(qrank.shape[0])
     if n < 2:
+        return
+    if typed:  # integer / float / array values: the reference's comparisons themselves (TypeError included)
+        verify_sort((TagSortableRecord.from_aligned_segment(r, tag_keys) for r in open_alignments(path, "rb")),
+                    tag_keys)
         return
     eng = E.get_engine(device)
     cols, dims, order = _key_columns(eng, keys, key_names, n)
@@ -554,10 +580,7 @@ def verify_bam_sort(path: str, tag_keys, device=None) -> None:
         return
 
     def record(j):
-        if len(tag_keys) <= 3:
-            vals = [key_names[k][int(keys[k][j])] for k in range(len(tag_keys))]
-        else:
-            vals = list(key_names[0][int(keys[0][j])])
+        vals = [key_names[k][int(keys[k][j])] for k in range(len(tag_keys))]
         return TagSortableRecord(tag_keys, vals, qnames[int(qrank[j])])
 
     raise _order_error(p + 1, record(p), record(p - 1))
@@ -576,7 +599,7 @@ def tag_sort_bam(in_bam: str, out_bam: str, tag_keys, device=None, level: int = 
     from sctools_amd import engine as E
 
     tag_keys = list(tag_keys)
-    keys, key_names, qrank, qnames = _sort_keys(in_bam, tag_keys)
+    keys, key_names, qrank, qnames, _ = _sort_keys(in_bam, tag_keys)
     n = int(qrank.shape[0])
     if n == 0:
         bamnative.write_order(in_bam, out_bam, np.zeros(0, np.int64), level=level)

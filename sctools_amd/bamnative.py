@@ -19,7 +19,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libsct_bam.so")
 
 OK, EIO, EFORMAT = 0, -1, -2
-KEYERROR, TYPEERROR, ZERODIV, VALUEERROR, EMPTY, MISSING_TAG = -10, -11, -12, -13, -14, -15
+KEYERROR, TYPEERROR, ZERODIV, VALUEERROR, EMPTY, MISSING_TAG, ETYPED = -10, -11, -12, -13, -14, -15, -16
+
+
+class TypedTagValue(Exception):
+    """A dictionary tag holds a float or array value (or, for the sort keys, an integer): the native
+    decoder cannot key it as the Python reader does, so the caller decodes with the Python reader
+    (include/sct_bam.h SCT_BAM_ETYPED)."""
 CELL_METRICS, GENE_METRICS, COUNT_MATRIX, SORT_KEYS = 0, 1, 2, 3
 _MODES = {"cell": CELL_METRICS, "gene": GENE_METRICS, "count": COUNT_MATRIX, "sortkeys": SORT_KEYS}
 EXPORTED = ("sct_bam_decode", "sct_bam_decode_tags", "sct_bam_last_error", "sct_bam_n", "sct_bam_column", "sct_bam_dictionary",
@@ -68,7 +74,7 @@ def available() -> bool:
 
 
 _EXC = {KEYERROR: KeyError, TYPEERROR: TypeError, ZERODIV: ZeroDivisionError, VALUEERROR: ValueError,
-        EMPTY: RuntimeError, EFORMAT: ValueError, EIO: OSError, MISSING_TAG: RuntimeError}
+        EMPTY: RuntimeError, EFORMAT: ValueError, EIO: OSError, MISSING_TAG: RuntimeError, ETYPED: TypedTagValue}
 
 
 def decode(path: str, metric_mode: str = "cell", threads: int = 0, tags=("CB", "UB", "GE")):

@@ -233,8 +233,11 @@ def columnarize(path: str, mode: str = "rb", metric_mode: str = MODE_CELL, nativ
     if native:
         if mode != "rb":
             raise ValueError("the native decoder reads BAM (mode 'rb')")
-        arrays, (cn, un, gn) = bamnative.decode(path, metric_mode)
-        return Columns(arrays, Dictionary(cn, True), Dictionary(un, True), Dictionary(gn, True))
+        try:
+            arrays, (cn, un, gn) = bamnative.decode(path, metric_mode)
+            return Columns(arrays, Dictionary(cn, True), Dictionary(un, True), Dictionary(gn, True))
+        except bamnative.TypedTagValue:  # float / array CB, UB or GE values: the Python reader keys them
+            pass
     cell_v, umi_v, gene_v, numeric = [], [], [], []
     is_cell = metric_mode == MODE_CELL
     prev_gene = object()

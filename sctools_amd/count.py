@@ -120,9 +120,11 @@ class CountMatrix:
         tags = (cell_barcode_tag or consts.CELL_BARCODE_TAG_KEY,
                 molecule_barcode_tag or consts.MOLECULE_BARCODE_TAG_KEY,
                 gene_name_tag or consts.GENE_NAME_TAG_KEY)
-        if open_mode == "rb":
+        try:
+            if open_mode != "rb":
+                raise bamnative.TypedTagValue("not BAM")
             arrays, (cells, umis, genes) = bamnative.decode(bam_file, "count", tags=tags)
-        else:
+        except bamnative.TypedTagValue:  # SAM, or float / array tag values: the Python reader
             arrays, (cells, umis, genes) = _python_columns(bam_file, open_mode, tags)
         gene_col = gene_columns(genes, gene_name_to_index)
         eng = engine.get_engine(device)

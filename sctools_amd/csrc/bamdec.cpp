@@ -67,6 +67,12 @@ struct Columns {
 };
 
 bool str_eq(const TagVal& a, const TagVal& b) { return a.n == b.n && memcmp(a.s, b.s, a.n) == 0; }
+// Python == of two present tag values of the kinds read_tag distinguishes
+bool val_eq(const TagVal& a, const TagVal& b) {
+  if (a.is_str || b.is_str) return a.is_str && b.is_str && str_eq(a, b);
+  if (a.raw || b.raw) return a.raw && b.raw && a.type == b.type && str_eq(a, b);
+  return a.i == b.i;
+}
 
 struct RecErr {
   int code = 0;
@@ -99,6 +105,20 @@ struct Parsed {
   uint8_t bits, xf;
   TagVal cb, ub, ge;
 };
+
+// A dictionary tag whose value the native path cannot key as the Python reader does: a float or
+// an array (any mode), or an integer where the order of the values matters (sort keys: Python
+// compares ints numerically, and an int with a str raises TypeError, bam.py:660-668).  The
+// caller then decodes with the Python reader (SCT_BAM_ETYPED).
+int typed_keys(const Parsed& o, bool ints, RecErr& e) {
+  for (const TagVal* v : {&o.cb, &o.ub, &o.ge})
+    if (v->present && (v->raw || (ints && !v->is_str))) {
+      e.code = SCT_BAM_ETYPED;
+      e.msg = std::string("a dictionary tag holds a value of type ") + v->type;
+      return -1;
+    }
+  return 0;
+}
 
 // One record (bytes after block_size).  Mirrors sctools_amd.columnar.record_fields.
 int parse_record(const uint8_t* d, uint32_t bs, bool is_cell, Parsed& o, RecErr& e) {
@@ -170,7 +190,7 @@ int parse_record(const uint8_t* d, uint32_t bs, bool is_cell, Parsed& o, RecErr&
         return -1;
       }
       // CR == CB compares the Python values: equal only for equal types and contents
-      if (cr.is_str == cb.is_str && (cr.is_str ? str_eq(cr, cb) : cr.i == cb.i)) bits |= B_PERFECT_CB;
+      if (val_eq(cr, cb)) bits |= B_PERFECT_CB;
     }
   } else if (cb.present) {
     bits |= B_HAS_CB;
@@ -185,7 +205,7 @@ int parse_record(const uint8_t* d, uint32_t bs, bool is_cell, Parsed& o, RecErr&
   } else if (uy.present && (uy.is_str ? uy.n > 0 : uy.i != 0)) {  // `if uyq:` on the default-"" value
     if (frac_counts(uy, &ug, &ul, e)) return -1;
   }
-  if (ur.present && ub.present && ur.is_str == ub.is_str && (ur.is_str ? str_eq(ur, ub) : ur.i == ub.i))
+  if (ur.present && ub.present && val_eq(ur, ub))
     bits |= B_PERFECT_UMI;
   // query_alignment_qualities (pysam 0.16)
   bool aq_none = l_seq == 0 || qual[0] == 0xFF;
@@ -262,7 +282,7 @@ int parse_record(const uint8_t* d, uint32_t bs, bool is_cell, Parsed& o, RecErr&
         return -1;
       }
     }
-    if (nh.present && !nh.is_str) nh_v = nh.i, nh_int = true;
+    if (nh.present && !nh.is_str && !nh.raw) nh_v = nh.i, nh_int = true;
     if (nh_int && nh_v == 1) bits |= B_NH1;
     uint64_t n_len = 0;
     for (uint32_t k = 0; k < n_cigar; k++) {
@@ -286,12 +306,13 @@ int parse_record(const uint8_t* d, uint32_t bs, bool is_cell, Parsed& o, RecErr&
   o.ref = ref, o.pos = pos, o.gq_sum = s, o.gq_len = q1 - q0, o.gq_gt30 = g;
   o.cy_gt30 = cg, o.cy_len = cl, o.uy_gt30 = ug, o.uy_len = ul, o.bits = bits, o.xf = x;
   o.cb = cb, o.ub = ub, o.ge = ge;
-  return 0;
+  return typed_keys(o, false, e);
 }
 
 // Count-matrix mode: the three dictionary tags (names in `tags`), XF and the query name; no
 // validation (count.py:222-270 reads only these, through has_tag / get_tag_or_default).
-int parse_count_record(const uint8_t* d, uint32_t bs, const char* tags, Parsed& o, const char** qname,
+// sortkeys: the TagSortBam / VerifyBamSort keys, where an integer value also counts as typed.
+int parse_count_record(const uint8_t* d, uint32_t bs, const char* tags, bool sortkeys, Parsed& o, const char** qname,
                        uint32_t* qlen, RecErr& e) {
   if (bs < 32) {
     e.code = SCT_BAM_EFORMAT;
@@ -337,7 +358,7 @@ int parse_count_record(const uint8_t* d, uint32_t bs, const char* tags, Parsed& 
   o.ref = (int32_t)rd32(d), o.pos = (int32_t)rd32(d + 4);
   o.gq_sum = o.gq_len = o.gq_gt30 = o.cy_gt30 = o.cy_len = o.uy_gt30 = o.uy_len = 0;
   o.bits = 0, o.xf = x;
-  return 0;
+  return typed_keys(o, sortkeys, e);
 }
 
 // Per-thread direct-mapped cache in front of the shared tables: cell-sorted input repeats
@@ -554,7 +575,7 @@ int sct_bam_decode_tags(const char* path, int32_t metric_mode, const char* tags,
         const uint32_t bs = rd32(buf.data() + starts[i]);
         const char* qn = nullptr;
         uint32_t qlen = 0;
-        if (generic ? parse_count_record(d, bs, tags, o, &qn, &qlen, e) : parse_record(d, bs, is_cell, o, e)) {
+        if (generic ? parse_count_record(d, bs, tags, sortkeys, o, &qn, &qlen, e) : parse_record(d, bs, is_cell, o, e)) {
           std::lock_guard<std::mutex> lk(err_m);
           if (base + i < first_bad.load()) {
             first_bad = base + i;

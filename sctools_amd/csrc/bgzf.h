@@ -116,68 +116,74 @@ class Interner {
 };
 
 // a tag's value as the Python reader sees it: a string (Z, H, A; integers printed in decimal
-// for the string tags) or an integer
+// for the string tags) or an integer; float and array values (f, d, B) keep their raw bytes
+// (`raw`: s, n), so that distinct values stay distinct where a value is only a key
 struct TagVal {
-  bool present = false, is_str = false;
+  bool present = false, is_str = false, raw = false;
+  char type = 0;
   const char* s = nullptr;
   size_t n = 0;
   int64_t i = 0;
   char num[24];
 };
 
-// Z/H/A/integer value at p (type t); returns the bytes the value occupies, or 0 for an
-// unknown type
+// Z/H/A/integer/float/array value at p (type t) within [p, end); returns the bytes the value
+// occupies, or 0 for an unknown type or a value running past `end` (a malformed record)
 inline size_t read_tag(const uint8_t* p, const uint8_t* end, char t, TagVal* v) {
+  const size_t room = end > p ? (size_t)(end - p) : 0;
+  size_t w = 0;
   switch (t) {
     case 'Z':
     case 'H': {
-      const uint8_t* z = (const uint8_t*)memchr(p, 0, end - p);
+      const uint8_t* z = room ? (const uint8_t*)memchr(p, 0, room) : nullptr;
       if (!z) return 0;
       if (v) v->present = true, v->is_str = true, v->s = (const char*)p, v->n = z - p;
+      if (v) v->type = t;
       return z - p + 1;
     }
     case 'A':
-      if (v) v->present = true, v->is_str = true, v->s = (const char*)p, v->n = 1;
+      if (room < 1) return 0;
+      if (v) v->present = true, v->is_str = true, v->s = (const char*)p, v->n = 1, v->type = t;
       return 1;
-    case 'c':
-      if (v) v->present = true, v->i = (int8_t)p[0];
-      return 1;
-    case 'C':
-      if (v) v->present = true, v->i = p[0];
-      return 1;
-    case 's':
-      if (v) v->present = true, v->i = (int16_t)rd16(p);
-      return 2;
-    case 'S':
-      if (v) v->present = true, v->i = rd16(p);
-      return 2;
-    case 'i':
-      if (v) v->present = true, v->i = (int32_t)rd32(p);
-      return 4;
-    case 'I':
-      if (v) v->present = true, v->i = rd32(p);
-      return 4;
-    case 'f':
-      if (v) v->present = true;
-      return 4;
-    case 'd':
-      if (v) v->present = true;
-      return 8;
+    case 'c': case 'C': w = 1; break;
+    case 's': case 'S': w = 2; break;
+    case 'i': case 'I': case 'f': w = 4; break;
+    case 'd': w = 8; break;
     case 'B': {
+      if (room < 5) return 0;
       const char sub = (char)p[0];
-      const uint32_t cnt = rd32(p + 1);
-      const size_t w = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
-      if (v) v->present = true;
-      return 5 + (size_t)cnt * w;
+      const size_t ew = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2
+                      : (sub == 'i' || sub == 'I' || sub == 'f') ? 4 : 0;
+      if (!ew) return 0;
+      const uint64_t len = 5 + (uint64_t)rd32(p + 1) * ew;
+      if (len > room) return 0;
+      if (v) v->present = true, v->raw = true, v->type = t, v->s = (const char*)p, v->n = (size_t)len;
+      return (size_t)len;
     }
     default:
       return 0;
   }
+  if (w > room) return 0;
+  if (v) {
+    v->present = true;
+    v->type = t;
+    switch (t) {
+      case 'c': v->i = (int8_t)p[0]; break;
+      case 'C': v->i = p[0]; break;
+      case 's': v->i = (int16_t)rd16(p); break;
+      case 'S': v->i = rd16(p); break;
+      case 'i': v->i = (int32_t)rd32(p); break;
+      case 'I': v->i = rd32(p); break;
+      default: v->raw = true, v->s = (const char*)p, v->n = w; break;  // f, d
+    }
+  }
+  return w;
 }
 
-// the string form of a value (the Python tag value passed through str())
+// the string form of an integer value (the Python tag value passed through str()); string and
+// raw values are left as they are
 inline void as_str(TagVal& v) {
-  if (!v.present || v.is_str) return;
+  if (!v.present || v.is_str || v.raw) return;
   snprintf(v.num, sizeof(v.num), "%lld", (long long)v.i);
   v.s = v.num;
   v.n = strlen(v.num);

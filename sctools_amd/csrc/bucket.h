@@ -96,9 +96,10 @@ __device__ __forceinline__ Work make_work(uint32_t id, uint32_t start, uint32_t 
   const uint32_t r = start + cnt - b;
   return Work{id, b, r < (uint32_t)kChunk ? r : (uint32_t)kChunk, 0u};
 }
-struct BucketCtl {  // device counters of one level (n_giant, n_big accumulate over levels)
-  uint32_t n_seg, n_work, n_giant, err;  // err: a mapped ref id >= 2^kRefBits (set by build_keys)
-  uint32_t n_big;
+struct BucketCtl {  // device counters of one level (n_giant, n_big, n_big_rec accumulate over levels)
+  uint32_t n_seg, n_work, n_rec;  // the next level's segments, work items and records
+  uint32_t n_giant, err;  // err: a mapped ref id >= 2^kRefBits (set by build_keys)
+  uint32_t n_big, n_big_rec;  // big buckets and their records
 };
 
 __device__ __forceinline__ uint64_t payload_w0(uint64_t key, int32_t ref, bool reverse, bool mapped, bool mito) {
@@ -110,19 +111,23 @@ __device__ __forceinline__ uint32_t payload_frag(uint64_t w0) {
   return (uint32_t)(w0 >> 2) & ((1u << kFragBits) - 1);
 }
 
+// ctr: the level's (n_seg, n_work, n_rec) counters
 __device__ __forceinline__ void push_segment(const Seg& sg, Seg* __restrict__ seg, Work* __restrict__ work,
-                                             BucketCtl* ctl) {
-  const uint32_t id = atomicAdd(&ctl->n_seg, 1u);
+                                             uint32_t* ctr) {
+  const uint32_t id = atomicAdd(&ctr[0], 1u);
+  atomicAdd(&ctr[2], sg.cnt);
   seg[id] = sg;
   const uint32_t nw = (sg.cnt + kChunk - 1) / kChunk;
-  const uint32_t w0 = atomicAdd(&ctl->n_work, nw);
+  const uint32_t w0 = atomicAdd(&ctr[1], nw);
   for (uint32_t k = 0; k < nw; k++) work[w0 + k] = make_work(id, sg.start, sg.cnt, k);
 }
 
-// level 0: small entities are terminal buckets, mid-sized ones big buckets; larger ones segments
+// level 0: small entities are terminal buckets, mid-sized ones big buckets; larger ones segments,
+// counted in seg_ctr (n_seg, n_work, n_rec)
 __global__ void k_bucket_level0(const int64_t* __restrict__ ent_start, int64_t n_ent, int64_t n,
                                 uint16_t* __restrict__ bdesc, uint32_t* __restrict__ bent, Seg* __restrict__ seg,
-                                Work* __restrict__ work, Seg* __restrict__ bigs, BucketCtl* ctl) {
+                                Work* __restrict__ work, Seg* __restrict__ bigs, BucketCtl* ctl,
+                                uint32_t* __restrict__ seg_ctr) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (e >= n_ent) return;
   const int64_t s0 = ent_start[e];
@@ -135,9 +140,10 @@ __global__ void k_bucket_level0(const int64_t* __restrict__ ent_start, int64_t n
   }
   if (c <= (uint32_t)kBigCap) {
     bigs[atomicAdd(&ctl->n_big, 1u)] = Seg{(uint32_t)s0, c, (uint32_t)e, 0u};
+    atomicAdd(&ctl->n_big_rec, c);
     return;
   }
-  push_segment(Seg{(uint32_t)s0, c, (uint32_t)e, 0u}, seg, work, ctl);
+  push_segment(Seg{(uint32_t)s0, c, (uint32_t)e, 0u}, seg, work, seg_ctr);
 }
 
 __global__ void __launch_bounds__(kBlock) k_bucket_hist(const uint64_t* __restrict__ keys, const Seg* __restrict__ seg,
@@ -306,25 +312,32 @@ __device__ __forceinline__ uint32_t split_flags(int Kb, int depth, int depth1, i
 // scan of the digit counts; the scatter's cursors) and their classification -- terminal
 // bucket, big bucket, giant, or next-level segment.  The block's new segments and work items are reserved
 // with one atomic each.
+// by_ent (level 1 planned before the key pass, segment.h k_level1_plan): the counts are per entity,
+// hist[entity][digit], and each is replaced by its child's start | kL1SegMark for the key pass;
+// the grid is an upper bound and *n_seg_dev the number of segments.
+constexpr uint32_t kL1SegMark = 0x80000000u;
 __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restrict__ seg,
-                                                            const uint32_t* __restrict__ hist,
+                                                            uint32_t* __restrict__ hist,
                                                             uint32_t* __restrict__ cur, int depth, int bits,
                                                             int K1, int KM, int KB, int parity, int by_ent,
                                                             uint16_t* __restrict__ bdesc, uint32_t* __restrict__ bent,
                                                             Seg* __restrict__ nseg, Work* __restrict__ nwork,
                                                             Seg* __restrict__ giants, Seg* __restrict__ bigs,
-                                                            BucketCtl* ctl) {
+                                                            BucketCtl* ctl, const uint32_t* __restrict__ n_seg_dev) {
   __shared__ uint32_t s_c[kRadix];
   __shared__ uint64_t s_scan[kWaves + 1];
   __shared__ uint32_t s_base[2];
+  if (n_seg_dev && blockIdx.x >= *n_seg_dev) return;  // block-uniform
   const int d = threadIdx.x;
   const size_t i = (size_t)blockIdx.x * kRadix + d;
   const Seg sg = seg[blockIdx.x];
-  const uint32_t c = hist[by_ent ? (size_t)sg.ent * kRadix + d : i];  // level 1: the key pass's per-entity counts
+  const size_t hi = by_ent ? (size_t)sg.ent * kRadix + d : i;
+  const uint32_t c = hist[hi];
   s_c[d] = c;
   uint64_t tot_c;
   const uint32_t start = sg.start + (uint32_t)block_exclusive_scan<uint64_t>((uint64_t)c, &tot_c, s_scan);
   cur[i] = start;
+  if (by_ent) hist[hi] = start | kL1SegMark;
   const int depth1 = depth + bits;
   uint32_t fl = 0;
   if (c) {
@@ -344,6 +357,7 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
     giants[id] = Seg{start, c, sg.ent, fl | par};
   } else if (big) {
     bigs[atomicAdd(&ctl->n_big, 1u)] = Seg{start, c, sg.ent, fl | par};
+    atomicAdd(&ctl->n_big_rec, c);
   }
   const uint32_t nw = push ? (c + kChunk - 1) / kChunk : 0u;
   // new segments and work items numbered by one scan of (segments << 32 | work items)
@@ -351,9 +365,12 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
   const uint64_t sw = block_exclusive_scan<uint64_t>(((uint64_t)(push ? 1 : 0) << 32) | nw, &tot_sw, s_scan);
   const uint32_t so = (uint32_t)(sw >> 32), wo = (uint32_t)sw;
   const uint64_t tot_s = tot_sw >> 32, tot_w = tot_sw & 0xffffffffull;
+  uint64_t tot_r;  // the new segments' records
+  (void)block_exclusive_scan<uint64_t>(push ? c : 0u, &tot_r, s_scan);
   if (d == 0 && tot_s) {
     s_base[0] = atomicAdd(&ctl->n_seg, (uint32_t)tot_s);
     s_base[1] = atomicAdd(&ctl->n_work, (uint32_t)tot_w);
+    atomicAdd(&ctl->n_rec, (uint32_t)tot_r);
   }
   __syncthreads();
   if (push) {

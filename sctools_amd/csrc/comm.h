@@ -60,6 +60,13 @@ int sct_comm_destroy(void* comm) {
   return SCT_OK;
 }
 
+int sct_comm_abort(void* comm) {
+  ::sct::last_error().clear();
+  if (!comm) return SCT_OK;
+  NCCLCHK(ncclCommAbort(static_cast<ncclComm_t>(comm)));
+  return SCT_OK;
+}
+
 int sct_allreduce_gene_partials(int64_t* partials, int64_t rows, void* comm, void* stream) {
   ::sct::last_error().clear();
   if (!comm) return ::sct::fail(SCT_EINVAL, "comm is NULL");

@@ -153,10 +153,10 @@ inline int radix_sort(const SortBuffers& B, int64_t n, int bits, int* which, hip
     const uint32_t* vin = cur ? B.vb : B.va;
     uint64_t* kout = cur ? B.ka : B.kb;
     uint32_t* vout = cur ? B.va : B.vb;
-    LAUNCH("radix_upsweep", k_radix_upsweep, dim3((unsigned)tiles), dim3(kBlock), s, kin, n, shift, tiles, B.counts);
+    LAUNCH_N("radix_upsweep", n, k_radix_upsweep, dim3((unsigned)tiles), dim3(kBlock), s, kin, n, shift, tiles, B.counts);
     int rc = scan_counts(B.counts, (int64_t)kRadix * tiles, B.offsets, B.sums, s);
     if (rc) return rc;
-    LAUNCH("radix_downsweep", k_radix_downsweep, dim3((unsigned)tiles), dim3(kBlock), s, kin, vin, kout, vout, n,
+    LAUNCH_N("radix_downsweep", n, k_radix_downsweep, dim3((unsigned)tiles), dim3(kBlock), s, kin, vin, kout, vout, n,
            shift, tiles, (const uint32_t*)B.offsets);
     cur ^= 1;
   }

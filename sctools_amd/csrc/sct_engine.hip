@@ -42,11 +42,11 @@ using namespace sct;
 
 namespace {
 
-constexpr int64_t kEntHistMax = 1 << 18;  // entities whose first-level histogram the key pass builds
+constexpr int64_t kEntHistMax = 1 << 18;  // entities whose first partition level is planned (k_level1_plan)
 
 struct Layout {
   size_t tile_cnt, scalars, scan_sums, keys_a, keys_b, vals_a, vals_b, counts, offsets, ent_start, partials;
-  size_t gcounts, gcursor, gtoff, gwork, dflags, gpay, seen, zero_mito, ent_hist;
+  size_t gcounts, gcursor, gtoff, gwork, dflags, gpay, seen, zero_mito, ent_hist, l1_toff, l1_tslot;
   size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, bigs, wctl, worder, total;
   int64_t num_tiles, num_chunks, max_ent, max_gene_work, max_seg, max_work;
   int n_buckets;
@@ -90,8 +90,12 @@ Layout layout_for(const sct_plan_t* plan) {
   L.gpay = take(L.gene ? sizeof(GenePayload) * (size_t)n1 : 0);
   L.seen = take(L.gene ? sizeof(uint32_t) * (size_t)(plan->n_cell_ids > 0 ? plan->n_cell_ids : 1) : 0);
   L.zero_mito = take(L.gene ? (size_t)(plan->n_gene_ids > 0 ? plan->n_gene_ids : 1) : 0);
-  // the key pass's first-level digit counts per entity (1 KB each; larger plans use k_bucket_hist)
-  L.ent_hist = take(L.max_ent <= kEntHistMax ? sizeof(uint32_t) * kRadix * (size_t)L.max_ent : 0);
+  // the planned first partition level (segment.h k_level1_plan): digit counts per entity (1 KB each;
+  // larger plans run level 1 as the other levels), each key-pass tile's offsets and slots
+  const bool l1 = L.max_ent <= kEntHistMax;
+  L.ent_hist = take(l1 ? sizeof(uint32_t) * kRadix * (size_t)L.max_ent : 0);
+  L.l1_toff = take(l1 ? sizeof(uint32_t) * kL1Slots * kRadix * (size_t)cdiv(n1, kKTile) : 0);
+  L.l1_tslot = take(l1 ? sizeof(uint2) * (size_t)cdiv(n1, kKTile) : 0);
   // bucket.h: segments have > kBCap records and are disjoint within a level (and giants overall)
   L.max_seg = n1 / (kBCap + 1) + 2;
   L.max_work = n1 / kChunk + L.max_seg + 2;
@@ -117,6 +121,9 @@ size_t count_bytes(const Layout& L) { return L.scalars + 256; }
 BucketCtl* bucket_ctl(void* ws, const Layout& L) {
   return reinterpret_cast<BucketCtl*>(at<uint64_t>(ws, L.scalars) + 8);
 }
+// level 0's (n_seg, n_work) when the first partition level is planned before the key pass
+uint32_t* level0_ctr(void* ws, const Layout& L) { return reinterpret_cast<uint32_t*>(at<uint64_t>(ws, L.scalars) + 12); }
+static_assert(sizeof(BucketCtl) <= 32, "BucketCtl at scalars + 64 B ends before the level-0 counters at + 96 B");
 
 int check_plan(const sct_plan_t* plan, const sct_records_t* rec) {
   if (!plan) return fail(SCT_EINVAL, "plan is NULL");
@@ -161,9 +168,9 @@ int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool du
   }
   HIPCHK(hipMemsetAsync(sc, 0, 2 * sizeof(uint64_t), s));
   if (((uintptr_t)ent & 15) == 0) {
-    LAUNCH("heads", k_heads4, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, (uint32_t)n_ids, sc + 1);
+    LAUNCH_N("heads", n, k_heads4, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, (uint32_t)n_ids, sc + 1);
   } else {
-    LAUNCH("heads", k_heads, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, (uint32_t)n_ids, sc + 1);
+    LAUNCH_N("heads", n, k_heads, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, (uint32_t)n_ids, sc + 1);
   }
   LAUNCH("scan", k_scan_wide, dim3(1), dim3(kScanWide), s, tc, tiles, sc);
   uint64_t host[2] = {0, 0};
@@ -179,26 +186,55 @@ int launch_hash_tile(bool cell, bool gene, dim3 grid, hipStream_t s, const uint1
                      const uint64_t* ka, const uint64_t* va, const uint64_t* kb, const uint64_t* vb, int64_t n,
                      const Bits& b, int64_t* partials, uint16_t* dflags) {
   if (cell && gene) {
-    LAUNCH("hash_tile", (k_hash_tile<true, true, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb, n,
+    LAUNCH_N("hash_tile", n, (k_hash_tile<true, true, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb, n,
            b, partials, dflags);
   } else if (cell) {
-    LAUNCH("hash_tile", (k_hash_tile<true, false, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb, n,
+    LAUNCH_N("hash_tile", n, (k_hash_tile<true, false, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb, n,
            b, partials, dflags);
   } else {
-    LAUNCH("hash_tile", (k_hash_tile<false, false, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb,
+    LAUNCH_N("hash_tile", n, (k_hash_tile<false, false, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb,
            n, b, partials, dflags);
   }
+  return SCT_OK;
+}
+
+// The first partition level planned before the key pass (segment.h k_level1_plan): run ids and
+// per-entity digit counts, level 0, then level 1's classification with a grid sized for the most
+// segments there can be (the device count bounds it): l1.hist then holds every segment child's start.
+// No host wait.
+int bucket_level1_plan(const Layout& L, void* ws, const KeyCols& kc, int64_t n, int64_t n_ent, const Bits& b,
+                       int64_t* ent_start, const L1Plan& l1, hipStream_t s) {
+  uint16_t* bdesc = at<uint16_t>(ws, L.bdesc);
+  uint32_t* bent = at<uint32_t>(ws, L.bent);
+  BucketCtl* ctl = bucket_ctl(ws, L);
+  uint32_t* ctr0 = level0_ctr(ws, L);
+  const int KB = b.k1 + b.k2 + b.h;
+  HIPCHK(hipMemsetAsync(bdesc, 0, sizeof(uint16_t) * (size_t)n, s));
+  HIPCHK(hipMemsetAsync(ctr0, 0, 3 * sizeof(uint32_t), s));
+  HIPCHK(hipMemsetAsync(l1.hist, 0, sizeof(uint32_t) * kRadix * (size_t)n_ent, s));
+  LAUNCH_N("level1_plan", n, k_level1_plan, dim3((unsigned)cdiv(n, kKTile)), dim3(kBlock), s, kc.ent, kc.k1, kc.n_k1, n,
+         (const uint64_t*)at<uint64_t>(ws, L.tile_cnt), b, b.k1 - kRadixBits, ent_start, l1);
+  LAUNCH("bucket_level0", k_bucket_level0, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, ent_start, n_ent, n,
+         bdesc, bent, at<Seg>(ws, L.seg_a), at<Work>(ws, L.work_a), at<Seg>(ws, L.bigs), ctl, ctr0);
+  const int64_t max_seg = n_ent < n / (kBigCap + 1) + 1 ? n_ent : n / (kBigCap + 1) + 1;
+  if (max_seg > L.max_seg) return fail(SCT_ENOMEM, "level 1: %lld segments exceed the workspace", (long long)max_seg);
+  LAUNCH("bucket_classify", k_bucket_classify, dim3((unsigned)max_seg), dim3(kBlock), s,
+         (const Seg*)at<Seg>(ws, L.seg_a), l1.hist, at<uint32_t>(ws, L.seg_cur), 0, kRadixBits, b.k1, b.k1 + b.k2, KB,
+         1, 1, bdesc, bent, at<Seg>(ws, L.seg_b), at<Work>(ws, L.work_b), at<Seg>(ws, L.giants), at<Seg>(ws, L.bigs),
+         ctl, (const uint32_t*)ctr0);
   return SCT_OK;
 }
 
 // bucket.h driver: level 0 classification, MSD levels until no segment exceeds kBCap, then
 // the hash-tile pass (+ giants).  One host wait per level to size the next level's launches,
 // for a copy queued right after the classification: the level's scatter runs meanwhile.
+// planned: level 0 and level 1 ran before the key pass (bucket_level1_plan), and the key pass wrote
+// the level-1 children: the loop starts at level 2.
 // Returns 1 (not an error code) when build_keys saw a mapped ref id the payload cannot hold:
 // the caller then reruns on the global-sort path.
 int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const int64_t* ent_start,
                     const uint8_t* mito, const Bits& b, bool cell, bool gene, int64_t* partials, uint16_t* dflags,
-                    const uint32_t* ehist, hipStream_t s) {
+                    bool planned, hipStream_t s) {
   if (n == 0) return SCT_OK;
   uint64_t* ka = at<uint64_t>(ws, L.keys_a);
   uint64_t* kb = at<uint64_t>(ws, L.keys_b);
@@ -213,17 +249,23 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   Seg* giants = at<Seg>(ws, L.giants);
   BucketCtl* ctl = bucket_ctl(ws, L);
   const int KB = b.k1 + b.k2 + b.h;
-  HIPCHK(hipMemsetAsync(bdesc, 0, sizeof(uint16_t) * (size_t)n, s));
   Seg* bigs = at<Seg>(ws, L.bigs);
-  HIPCHK(hipMemsetAsync(ctl, 0, 3 * sizeof(uint32_t), s));  // keeps ctl->err from build_keys
-  HIPCHK(hipMemsetAsync(&ctl->n_big, 0, sizeof(uint32_t), s));
-  LAUNCH("bucket_level0", k_bucket_level0, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, ent_start, n_ent, n,
-         bdesc, bent, seg[0], work[0], bigs, ctl);
+  int depth = 0, level = 1, c = 0;
+  if (planned) {
+    depth = KB < kRadixBits ? KB : kRadixBits;
+    level = 2;
+    c = 1;
+  } else {
+    HIPCHK(hipMemsetAsync(bdesc, 0, sizeof(uint16_t) * (size_t)n, s));
+    HIPCHK(hipMemsetAsync(ctl, 0, offsetof(BucketCtl, err), s));  // keeps ctl->err from build_keys
+    HIPCHK(hipMemsetAsync(&ctl->n_big, 0, 2 * sizeof(uint32_t), s));
+    LAUNCH("bucket_level0", k_bucket_level0, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, ent_start, n_ent,
+           n, bdesc, bent, seg[0], work[0], bigs, ctl, &ctl->n_seg);
+  }
   BucketCtl h{};
   if (int rb = readback(&h, ctl, sizeof(h), s)) return rb;
   if (h.err & 2) return fail(SCT_EINVAL, "a gene / cell / umi id lies outside its dictionary size");
   if (h.err) return 1;
-  int depth = 0, level = 1, c = 0;
   while (h.n_seg > 0) {
     if ((int64_t)h.n_seg > L.max_seg || (int64_t)h.n_work > L.max_work)
       return fail(SCT_ENOMEM, "bucket level %d: %u segments / %u work items exceed the workspace", level, h.n_seg,
@@ -235,21 +277,17 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     const uint64_t* vin = src ? vb : va;
     uint64_t* kout = src ? ka : kb;
     uint64_t* vout = src ? va : vb;
-    // level 1's segments are entities: the key pass counted their digits (ehist)
-    const bool by_ent = level == 1 && ehist != nullptr;
-    if (!by_ent) {
-      HIPCHK(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kRadix * (size_t)h.n_seg, s));
-      LAUNCH("bucket_hist", k_bucket_hist, dim3(h.n_work), dim3(kBlock), s, kin, (const Seg*)seg[c],
-             (const Work*)work[c], shift, bits, hist);
-    }
-    HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), s));  // next level's n_seg, n_work
-    LAUNCH("bucket_classify", k_bucket_classify, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c],
-           by_ent ? ehist : (const uint32_t*)hist, cur, depth, bits, b.k1, b.k1 + b.k2, KB, level & 1, by_ent ? 1 : 0,
-           bdesc, bent, seg[c ^ 1], work[c ^ 1], giants, bigs, ctl);
+    HIPCHK(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kRadix * (size_t)h.n_seg, s));
+    LAUNCH_N("bucket_hist", h.n_rec, k_bucket_hist, dim3(h.n_work), dim3(kBlock), s, kin, (const Seg*)seg[c],
+           (const Work*)work[c], shift, bits, hist);
+    HIPCHK(hipMemsetAsync(ctl, 0, 3 * sizeof(uint32_t), s));  // next level's n_seg, n_work, n_rec
+    LAUNCH("bucket_classify", k_bucket_classify, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c], hist, cur, depth,
+           bits, b.k1, b.k1 + b.k2, KB, level & 1, 0, bdesc, bent, seg[c ^ 1], work[c ^ 1], giants, bigs, ctl,
+           (const uint32_t*)nullptr);
     // the next level's counts are final after classify: read them while the scatter runs
     if (int rb = readback_start(ctl, sizeof(h), s)) return rb;
     const uint32_t n_work = h.n_work;
-    LAUNCH("bucket_scatter", k_bucket_scatter, dim3(n_work), dim3(kSBlock), s, kin, vin, kout, vout,
+    LAUNCH_N("bucket_scatter", h.n_rec, k_bucket_scatter, dim3(n_work), dim3(kSBlock), s, kin, vin, kout, vout,
            (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
     if (int rb = readback_finish(&h, sizeof(h))) return rb;
     c ^= 1;
@@ -268,7 +306,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     const dim3 bgrid(h.n_big);
     const bool wide = b.k1 > kNarrowK1Bits;
 #define SCT_BIG(C, G, W)                                                                                          \
-  LAUNCH("big_bucket", (k_big_bucket<C, G, W>), bgrid, dim3(kBigBlock), s, (const Seg*)bigs, ka, va, kb, vb, b, \
+  LAUNCH_N("big_bucket", h.n_big_rec, (k_big_bucket<C, G, W>), bgrid, dim3(kBigBlock), s, (const Seg*)bigs, ka, va, kb, vb, b, \
          partials, dflags)
     if (cell && gene) {
       if (wide) { SCT_BIG(true, true, true); } else { SCT_BIG(true, true, false); }
@@ -302,17 +340,17 @@ template <bool kBucket, bool kStreams>
 int launch_build_keys(bool cell, bool gene, dim3 grid, hipStream_t s, const KeyCols& kc, const RecCols& rc2,
                       const uint8_t* mito, int64_t n, const uint64_t* toff, const Bits& b, uint64_t* keys,
                       void* vals, int64_t* ent_start, int64_t* partials, uint32_t* gcounts, int n_buckets,
-                      uint32_t* err, uint32_t* gwide, uint32_t* gtoff, uint32_t* ent_hist) {
+                      uint32_t* err, uint32_t* gwide, uint32_t* gtoff, const L1Plan& l1) {
   if (cell && gene) {
-    LAUNCH_SHM("build_keys", (k_build_keys_run<true, true, kBucket, kStreams>), grid, dim3(kBlock),
+    LAUNCH_SHM_N("build_keys", n, (k_build_keys_run<true, true, kBucket, kStreams>), grid, dim3(kBlock),
                sizeof(uint32_t) * (size_t)n_buckets, s, kc, rc2, mito, n, toff, b, keys, vals, ent_start, partials,
-               gcounts, n_buckets, err, gwide, gtoff, ent_hist);
+               gcounts, n_buckets, err, gwide, gtoff, l1);
   } else if (cell) {
-    LAUNCH("build_keys", (k_build_keys_run<true, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito, n,
-           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide, gtoff, ent_hist);
+    LAUNCH_N("build_keys", n, (k_build_keys_run<true, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito, n,
+           toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide, gtoff, l1);
   } else {
-    LAUNCH("build_keys", (k_build_keys_run<false, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito,
-           n, toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide, gtoff, ent_hist);
+    LAUNCH_N("build_keys", n, (k_build_keys_run<false, false, kBucket, kStreams>), grid, dim3(kBlock), s, kc, rc2, mito,
+           n, toff, b, keys, vals, ent_start, partials, gcounts, n_buckets, err, gwide, gtoff, l1);
   }
   return SCT_OK;
 }
@@ -378,9 +416,15 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   int64_t* partials = at<int64_t>(ws, L.partials);
   uint32_t* gcounts = gene ? at<uint32_t>(ws, L.gcounts) : nullptr;
   uint32_t* gtoff = gene ? at<uint32_t>(ws, L.gtoff) : nullptr;
-  // bucket path: the key pass counts the first partition level's digits per entity
-  uint32_t* ehist = bucket && L.max_ent <= kEntHistMax && n_ent > 0 ? at<uint32_t>(ws, L.ent_hist) : nullptr;
-  if (ehist) HIPCHK(hipMemsetAsync(ehist, 0, sizeof(uint32_t) * kRadix * (size_t)n_ent, s));
+  // bucket path: the first partition level planned before the key pass when its digit comes from
+  // k1 alone (segment.h k_level1_plan), so the key pass writes the level-1 children itself
+  const char* nol1 = getenv("SCT_NO_L1_PLAN");
+  const bool planned = bucket && L.max_ent <= kEntHistMax && n_ent > 0 && b.k1 >= kRadixBits &&
+                       !(nol1 && nol1[0] == '1');
+  L1Plan l1{};
+  if (planned)
+    l1 = L1Plan{at<uint32_t>(ws, L.ent_hist), at<uint32_t>(ws, L.l1_toff), at<uint2>(ws, L.l1_tslot), B.kb,
+                at<uint64_t>(ws, L.vals_b)};
   const uint8_t* mito = gene_is_mito;
   if (cell && !mito) {
     uint8_t* z = at<uint8_t>(ws, L.zero_mito);
@@ -397,6 +441,10 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   const bool streams = exact && out_i;
   BucketCtl* ctl = bucket_ctl(ws, L);
   HIPCHK(hipMemsetAsync(ctl, 0, sizeof(BucketCtl), s));
+  if (planned) {
+    rc = bucket_level1_plan(L, ws, kc, n, n_ent, b, ent_start, l1, s);
+    if (rc) return rc;
+  }
   // gene payload format: narrow (8 B) unless an operand does not fit (checked by the exact-stream
   // pass; without it the wide format is used)
   uint32_t* gwide = reinterpret_cast<uint32_t*>(at<uint64_t>(ws, L.scalars) + 16);
@@ -404,16 +452,16 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   if (bucket) {
     uint64_t* va = at<uint64_t>(ws, L.vals_a);
     rc = streams ? launch_build_keys<true, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
-                                                 partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff, ehist)
+                                                 partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff, l1)
                  : launch_build_keys<true, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
-                                                  partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff, ehist);
+                                                  partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff, l1);
   } else {
     rc = streams ? launch_build_keys<false, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
                                                   ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff,
-                                                  nullptr)
+                                                  l1)
                  : launch_build_keys<false, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
                                                    ent_start, partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff,
-                                                   nullptr);
+                                                   l1);
     if (rc) return rc;
     uint32_t err = 0;  // the bucket path reads the flag at its first level sync
     if (int rb = readback(&err, &ctl->err, sizeof(err), s)) return rb;
@@ -424,7 +472,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   // 2-3. distinct counts (+ per-record distinct events for the gene view)
   uint16_t* dflags = gene ? at<uint16_t>(ws, L.dflags) : nullptr;
   if (bucket) {
-    rc = bucket_distinct(L, ws, n, n_ent, ent_start, mito, b, cell, gene, partials, dflags, ehist, s);
+    rc = bucket_distinct(L, ws, n, n_ent, ent_start, mito, b, cell, gene, partials, dflags, planned, s);
     if (rc == 1)  // a mapped ref id does not fit the bucket payload: redo on the global-sort path
       return pipeline(plan, rec, gene_is_mito, ws, ws_bytes, out_i, out_f, capacity, n_rows, gene_partials, s,
                       false);
@@ -437,13 +485,13 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     const uint32_t* vals = which ? B.vb : B.va;
     const dim3 rgrid((unsigned)cdiv(n, kReduceTile));
     if (cell && gene) {
-      LAUNCH("reduce_sorted", (k_reduce_sorted<true, true>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
+      LAUNCH_N("reduce_sorted", n, (k_reduce_sorted<true, true>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
              partials, dflags);
     } else if (cell) {
-      LAUNCH("reduce_sorted", (k_reduce_sorted<true, false>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
+      LAUNCH_N("reduce_sorted", n, (k_reduce_sorted<true, false>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
              partials, dflags);
     } else {
-      LAUNCH("reduce_sorted", (k_reduce_sorted<false, false>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
+      LAUNCH_N("reduce_sorted", n, (k_reduce_sorted<false, false>), rgrid, dim3(kBlock), s, keys, vals, n, rc2, mito, b,
              partials, dflags);
     }
   }
@@ -484,11 +532,11 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     LAUNCH_SHM("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), 2 * sizeof(uint32_t) * (size_t)(L.n_buckets + 1), s,
                (const uint32_t*)gcounts, L.n_buckets, gcur, gwork, n_gwork);
     static_assert(kEmitTile == kKTile, "gene_emit tiles are the key pass's tiles (gtoff)");
-    LAUNCH_SHM("gene_emit", k_gene_emit, dim3((unsigned)cdiv(n, kEmitTile)), dim3(kBlock),
+    LAUNCH_SHM_N("gene_emit", n, k_gene_emit, dim3((unsigned)cdiv(n, kEmitTile)), dim3(kBlock),
                2 * sizeof(uint32_t) * (size_t)L.n_buckets, s, rec->gene, rc2, (const uint16_t*)dflags, n,
                (const uint32_t*)gcur, (const uint32_t*)gtoff, L.n_buckets, (const uint32_t*)gwide, gpay);
     HIPCHK(hipMemsetAsync(gene_partials, 0, sizeof(int64_t) * SCT_NP * (size_t)plan->n_gene_ids, s));
-    LAUNCH("gene_reduce", k_gene_reduce, dim3((unsigned)L.max_gene_work), dim3(kBlock), s, (const void*)gpay,
+    LAUNCH_N("gene_reduce", n, k_gene_reduce, dim3((unsigned)L.max_gene_work), dim3(kBlock), s, (const void*)gpay,
            (const int64_t*)gwork, (const int64_t*)n_gwork, plan->n_gene_ids, (const uint32_t*)gwide, gene_partials);
   }
   if (n_rows) *n_rows = n_ent;
@@ -627,7 +675,7 @@ int sct_profile_only(const char* kernel_name) {
   return SCT_OK;
 }
 
-int sct_profile_read(const char** names, double* ms, int64_t* launches, int max_kernels) {
+int sct_profile_read_items(const char** names, double* ms, int64_t* launches, int64_t* items, int max_kernels) {
   // waits for the recorded events, returns per-kernel totals, and resets the counters
   static thread_local std::vector<std::string> held;
   held.clear();
@@ -645,6 +693,7 @@ int sct_profile_read(const char** names, double* ms, int64_t* launches, int max_
     if (k < max_kernels) {
       if (ms) ms[k] = tot;
       if (launches) launches[k] = (int64_t)e.ev.size();
+      if (items) items[k] = e.items;
     }
     k++;
   }
@@ -652,6 +701,10 @@ int sct_profile_read(const char** names, double* ms, int64_t* launches, int max_
     if (names) names[i] = held[i].c_str();
   prof_entries().clear();
   return k;
+}
+
+int sct_profile_read(const char** names, double* ms, int64_t* launches, int max_kernels) {
+  return sct_profile_read_items(names, ms, launches, nullptr, max_kernels);
 }
 
 int sct_workspace_size(const sct_plan_t* plan, size_t* bytes) {
@@ -776,14 +829,14 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
       const int shift = ps * kRadixBits;
       const bool first = ps == 0, last = ps == passes - 1;
       const int32_t* hkey = first ? in->cell : keys[(ps - 1) & 1];
-      LAUNCH("tag_row_hist", k_row_hist, dim3((unsigned)tiles), dim3(kBlock), s, hkey, n, shift, tiles, counts);
+      LAUNCH_N("tag_row_hist", n, k_row_hist, dim3((unsigned)tiles), dim3(kBlock), s, hkey, n, shift, tiles, counts);
       rc = scan_counts(counts, (int64_t)kRadix * tiles, offsets, sums, s);
       if (rc) return rc;
       const uint4* rin = first ? nullptr : rows[(ps - 1) & 1];
       uint4* rout = rows[ps & 1];
       int32_t* kout = keys[ps & 1];
 #define SCT_ROWS(A, Z)                                                                                              \
-  LAUNCH("tag_row_scatter", (k_row_scatter<A, Z>), dim3((unsigned)tiles), dim3(kBlock), s, *in, rin, rout, kout, \
+  LAUNCH_N("tag_row_scatter", n, (k_row_scatter<A, Z>), dim3((unsigned)tiles), dim3(kBlock), s, *in, rin, rout, kout, \
          *out, n, shift, tiles, (const uint32_t*)offsets)
       if (first && last) {
         SCT_ROWS(true, true);
@@ -802,7 +855,7 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
                 at<uint32_t>(workspace, L.vb), at<uint32_t>(workspace, L.counts), at<uint32_t>(workspace, L.offsets),
                 at<uint64_t>(workspace, L.sums)};
   const dim3 grid((unsigned)cdiv(n, kBlock));
-  LAUNCH("tag_pack", k_pack, grid, dim3(kBlock), s, *in, recs);
+  LAUNCH_N("tag_pack", n, k_pack, grid, dim3(kBlock), s, *in, recs);
   int field_bits = 0;
   for (int i = 0; i < nf - (tiebreak ? 1 : 0); i++) field_bits += f[i].bits;
   if (tiebreak && field_bits <= 64) {
@@ -815,7 +868,7 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
     int th = (field_bits + kRadixBits - 1) / kRadixBits * kRadixBits - field_bits;  // free bits of the last digit
     if (th > tie_top) th = tie_top;
     if (field_bits + th > 64) th = 64 - field_bits;
-    LAUNCH("tag_keys", k_field_keys, grid, dim3(kBlock), s, *in, n, rk, tiebreak, tie_top, th, B.ka, B.va);
+    LAUNCH_N("tag_keys", n, k_field_keys, grid, dim3(kBlock), s, *in, n, rk, tiebreak, tie_top, th, B.ka, B.va);
     int which = 0;
     rc = radix_sort(B, n, field_bits + th, &which, s);
     if (rc) return rc;
@@ -840,7 +893,7 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
       LAUNCH("tag_long_scatter", k_long_scatter, dim3((unsigned)cdiv(h[1], kBlock)), dim3(kBlock), s,
              (const uint32_t*)pos_of, (const uint32_t*)(w2 ? LB.vb : LB.va), (int64_t)h[1], perm);
     }
-    LAUNCH("tag_unpack", k_unpack, grid, dim3(kBlock), s, (const uint4*)recs, (const uint32_t*)perm, n, *out);
+    LAUNCH_N("tag_unpack", n, k_unpack, grid, dim3(kBlock), s, (const uint4*)recs, (const uint32_t*)perm, n, *out);
     return SCT_OK;
   }
   // rounds: fields from the least significant end, packed greedily into <= 64-bit keys
@@ -853,14 +906,14 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
     rk.nf = hi - lo;
     rk.bits = bits;
     for (int i = 0; i < rk.nf; i++) rk.f[i] = f[lo + i];
-    LAUNCH("tag_keys", k_round_keys, grid, dim3(kBlock), s, (const uint4*)recs, tiebreak, perm, n, rk, B.ka, B.va);
+    LAUNCH_N("tag_keys", n, k_round_keys, grid, dim3(kBlock), s, (const uint4*)recs, tiebreak, perm, n, rk, B.ka, B.va);
     int which = 0;
     rc = radix_sort(B, n, bits, &which, s);
     if (rc) return rc;
     perm = which ? B.vb : B.va;
     hi = lo;
   }
-  LAUNCH("tag_unpack", k_unpack, grid, dim3(kBlock), s, (const uint4*)recs, perm, n, *out);
+  LAUNCH_N("tag_unpack", n, k_unpack, grid, dim3(kBlock), s, (const uint4*)recs, perm, n, *out);
   return SCT_OK;
 }
 

@@ -207,6 +207,110 @@ __device__ __forceinline__ int64_t tile_run_ids(const int32_t* __restrict__ ent,
   return ebase;
 }
 
+// ---- the first partition level, planned before the key pass (bucket.h) ----
+// Level-0 segments are entities of more than kBigCap records (k_bucket_level0).  Their first
+// partition level is planned from the entity and k1 columns alone, so that the key pass writes
+// every payload of a segment straight into its level-1 child instead of writing it in input order
+// for k_bucket_scatter to move once more (aggregator.py:264, 300-303: the molecule and fragment
+// Counters this grouping serves):
+//   k_level1_plan      per key-pass tile: run ids (ent_start), each record's level-1 digit counted
+//                      per (entity, digit) in l1.hist (the children's sizes), and the tile's range
+//                      inside every child it feeds, reserved with one atomic per (slot, digit): l1.toff;
+//   k_bucket_classify  (level 1) turns l1.hist into the children's starts, in place, marked kL1Seg;
+//   k_build_keys_run   ranks each segment record inside its tile's range with one LDS atomic.
+// Only runs that can be segments get a slot: the tile's first and last runs and the runs of more
+// than kBigCap records inside it (at most two: a tile holds kKTile < 3 (kBigCap + 1) records).
+// The digit is the top kRadixBits of key' = [k1' | k2 | hash]; the host takes this path when they
+// come from k1' alone (k1 >= kRadixBits bits): digit = k1' >> (k1 - kRadixBits).
+constexpr int kL1Slots = 4;
+constexpr uint32_t kL1NoSlot = 0xffffu;
+constexpr uint32_t kL1Seg = kL1SegMark;  // l1.hist entry of a classified segment: child start | kL1Seg
+static_assert(kKTile < 3 * (kBigCap + 1) + 2, "at most two inner segment runs per key-pass tile");
+struct L1Plan {
+  uint32_t* hist;  // [entity][kRadix] (nullptr: payloads are written in input order)
+  uint32_t* toff;  // [tile][kL1Slots][kRadix]: the tile's offset inside each child it feeds
+  uint2* tslot;    // [tile]: the slots' local run ids, 16 bits each (kL1NoSlot: none)
+  uint64_t* keys_b;  // the level-1 children's buffer (B)
+  uint64_t* vals_b;
+};
+__device__ __forceinline__ uint32_t l1_slot_loc(uint2 ts, int k) {
+  return ((k < 2 ? ts.x : ts.y) >> (16 * (k & 1))) & 0xffffu;
+}
+
+template <int kN>
+__device__ __forceinline__ int slot_of(uint32_t loc, const uint32_t (&sl)[kN]) {
+  int r = -1;
+#pragma unroll
+  for (int k = kN - 1; k >= 0; k--) r = loc == sl[k] ? k : r;
+  return r;
+}
+
+__global__ void __launch_bounds__(kBlock) k_level1_plan(const int32_t* __restrict__ ent, const int32_t* __restrict__ k1col,
+                                                        uint32_t n_k1, int64_t n, const uint64_t* __restrict__ tile_off,
+                                                        Bits b, int dshift, int64_t* __restrict__ ent_start,
+                                                        L1Plan l1) {
+  __shared__ uint16_t s_e16[kTilePad];
+  __shared__ uint64_t s_scan[kWaves + 1];
+  __shared__ uint64_t s_hb[kKTile / 64];
+  __shared__ uint32_t s_h[kL1Slots * kRadix];
+  __shared__ uint32_t s_slot[kL1Slots];
+  __shared__ uint32_t s_nmid;
+  static_assert(kBlock == kRadix, "one thread per digit");
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kKTile;
+  const int tile_n = (int)((n - base) < kKTile ? (n - base) : kKTile);
+  for (int i = t; i < kL1Slots * kRadix; i += kBlock) s_h[i] = 0;
+  if (t < kL1Slots) s_slot[t] = kL1NoSlot;
+  if (t == 0) s_nmid = 0;
+  uint32_t heads, ex, n_heads;  // (tile_run_ids' barriers publish the initialisation above)
+  const int64_t ebase = tile_run_ids(ent, base, tile_n, tile_off[(size_t)blockIdx.x * kKTilesPerBlock], s_e16, s_hb,
+                                     s_scan, ent_start, &heads, &ex, &n_heads);
+  const uint32_t first = s_e16[epad(0)];  // the run at the tile's first position
+  // inner runs with more than kBigCap records in the tile: head h and position h + kBigCap in one run
+  for (uint32_t hb = heads; hb; hb &= hb - 1) {
+    const int j = __ffs(hb) - 1;
+    const uint32_t l = ex + (uint32_t)__popc(heads & ((2u << j) - 1u));
+    const int h = t * kKItems + j;
+    if (l != first && l != n_heads && h + kBigCap < tile_n && s_e16[epad(h + kBigCap)] == l) {
+      const uint32_t k = atomicAdd(&s_nmid, 1u);
+      if (k < kL1Slots - 2) s_slot[1 + k] = l;
+    }
+  }
+  if (t == 0) {
+    s_slot[0] = first;
+    if (n_heads != first) s_slot[kL1Slots - 1] = n_heads;
+  }
+  __syncthreads();
+  uint32_t sl[kL1Slots];
+#pragma unroll
+  for (int k = 0; k < kL1Slots; k++) sl[k] = s_slot[k];
+  for (int j0 = 0; j0 < kKItems; j0 += kRunBatch) {  // striped, loads of kRunBatch rounds in flight
+    uint32_t v[kRunBatch];
+#pragma unroll
+    for (int u = 0; u < kRunBatch; u++) {
+      const int q = (j0 + u) * kBlock + t;
+      v[u] = (uint32_t)k1col[base + (q < tile_n ? q : 0)];
+    }
+#pragma unroll
+    for (int u = 0; u < kRunBatch; u++) {
+      const int q = (j0 + u) * kBlock + t;
+      if (q >= tile_n) continue;
+      const uint32_t k1 = v[u] < n_k1 ? v[u] : 0u;  // the key pass's rule for an invalid id
+      const int k = slot_of(s_e16[epad(q)], sl);
+      if (k >= 0) atomicAdd(&s_h[k * kRadix + (b.scramble(k1) >> dshift)], 1u);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kL1Slots; k++) {
+    const uint32_t c = s_h[k * kRadix + t];
+    if (sl[k] != kL1NoSlot && c)
+      l1.toff[((size_t)blockIdx.x * kL1Slots + k) * kRadix + t] =
+          atomicAdd(&l1.hist[(size_t)(ebase + sl[k]) * kRadix + t], c);
+  }
+  if (t == 0) l1.tslot[blockIdx.x] = make_uint2(sl[0] | (sl[1] << 16), sl[2] | (sl[3] << 16));
+}
+
 // Exact-lane increments of RN(a / B) for one denominator B per barcode stream and tile (the tile's
 // first record's): a sample with that denominator adds 8 table words instead of computing them
 // (fx_increments).  Barcode lengths are fixed in a chemistry; any other denominator is computed
@@ -362,11 +466,12 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
 }
 
 // kBucket: write the bucket path's 16-byte payload (bucket.h: w0 = key' | ref | strand |
-// mapped, w1 = index | pos; a mapped ref id >= 2^kRefBits raises *err).  Otherwise the
-// global sort's (key with entity bits, u32 value with bit 31 = unmapped).
+// mapped, w1 = index | pos; a mapped ref id >= 2^kRefBits raises *err): a segment's record (l1.hist
+// set: the first partition level planned by k_level1_plan) straight into its level-1 child in buffer
+// B, any other record at its own position in buffer A.  Otherwise the global sort's (key with entity
+// bits, u32 value with bit 31 = unmapped).
 // kStreams: also the exact quality-stream lanes of the runs (stream_tile), reusing the tile's
 // run ids: the stream ALU work overlaps the key pass's memory traffic in one launch.
-constexpr int kDhRuns = 5;  // LDS digit-count slots: the tile's first 4 runs and its last
 constexpr int kKeyBatch = 4;  // striped rounds whose column loads are issued together (8: occupancy 3, slower)
 static_assert(kKItems % kKeyBatch == 0, "whole batches");
 
@@ -379,7 +484,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
                                                            int64_t* __restrict__ partials,
                                                            uint32_t* __restrict__ gene_counts, int n_buckets,
                                                            uint32_t* __restrict__ err, uint32_t* __restrict__ gwide,
-                                                           uint32_t* __restrict__ gtoff, uint32_t* __restrict__ ent_hist) {
+                                                           uint32_t* __restrict__ gtoff, L1Plan l1) {
   static_assert(!kGene || kCell, "gene buckets come from the cell view");
   __shared__ uint16_t s_e16[kTilePad];
   __shared__ uint64_t s_scan[kWaves + 1];
@@ -398,26 +503,38 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
     fill_rcp(s_rcp);
     fill_stream_tabs<kCell>(r, base, s_tab);
   }
-  // the first partition level's digit histogram per entity (bucket.h; ent_hist set on the bucket
-  // path): the tile's first kDhRuns runs count in LDS, later ones with global atomics
-  __shared__ uint32_t s_dh[kBucket ? kDhRuns * kRadix : 1];
+  // level-1 children (l1.hist set): per slot whose run is a segment, the next position of each
+  // child inside this tile's range; s_lslot = the slot's local run id, or kL1NoSlot
+  __shared__ uint32_t s_pos[kBucket ? kL1Slots * kRadix : 1];
+  __shared__ uint32_t s_lslot[kL1Slots];
   const int KB = b.k1 + b.k2 + b.h;
   const int bits1 = KB < kRadixBits ? KB : kRadixBits;
   const int sh1 = KB - bits1;
+  const uint64_t tile_off0 = tile_off[(size_t)blockIdx.x * kKTilesPerBlock];
   if constexpr (kBucket) {
-    if (ent_hist)
-      for (int i = t; i < kDhRuns * kRadix; i += kBlock) s_dh[i] = 0;
+    if (l1.hist) {
+      static_assert(kBlock == kRadix, "one thread per digit");
+      const uint2 ts = l1.tslot[blockIdx.x];
+#pragma unroll
+      for (int k = 0; k < kL1Slots; k++) {
+        const uint32_t l = l1_slot_loc(ts, k);
+        bool seg = false;
+        if (l != kL1NoSlot) {
+          const uint32_t v = l1.hist[(size_t)((int64_t)tile_off0 - 1 + l) * kRadix + t];
+          seg = (v & kL1Seg) != 0;  // every digit of a classified segment carries the mark
+          if (seg) s_pos[k * kRadix + t] = (v & ~kL1Seg) + l1.toff[((size_t)blockIdx.x * kL1Slots + k) * kRadix + t];
+        }
+        if (t == 0) s_lslot[k] = seg ? l : kL1NoSlot;
+      }
+    }
   }
   // 1-2. run index of every record of the tile
   uint32_t my_heads, my_ex, n_heads;
-  const int64_t ebase = tile_run_ids(c.ent, base, tile_n, tile_off[(size_t)blockIdx.x * kKTilesPerBlock], s_e16,
-                                     s_hb, s_scan, ent_start, &my_heads, &my_ex, &n_heads);
-  // first-level digit counts: LDS slots for the tile's first kDhRuns - 1 runs and its last run
-  // (the runs that may continue into a neighbouring tile); runs wholly inside the tile (rarely
-  // segments) count with global atomics
-  const auto dh_slot = [n_heads](int64_t loc) -> int {
-    return loc < kDhRuns - 1 ? (int)loc : (loc == (int64_t)n_heads ? kDhRuns - 1 : -1);
-  };
+  const int64_t ebase = tile_run_ids(c.ent, base, tile_n, tile_off0, s_e16, s_hb, s_scan,
+                                     (kBucket && l1.hist) ? nullptr : ent_start, &my_heads, &my_ex, &n_heads);
+  uint32_t lsl[kL1Slots];
+#pragma unroll
+  for (int k = 0; k < kL1Slots; k++) lsl[k] = (kBucket && l1.hist) ? s_lslot[k] : kL1NoSlot;
 
   // 3. striped pass: keys, values and the run's additive metrics.  Runs are contiguous, so
   // in a round the wave's lanes cross a run boundary together: flush wave-cooperatively.
@@ -473,7 +590,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
       uint32_t k2 = (uint32_t)vk2[u];
       if (k1 >= c.n_k1 || k2 >= c.n_k2) {  // invalid input: reported, never used as an index
         atomicOr(err, 2u);
-        k1 = k2 = 0;
+        k1 = k1 < c.n_k1 ? k1 : 0u;  // (k_level1_plan applies the same rule to k1)
+        k2 = k2 < c.n_k2 ? k2 : 0u;
       }
       const uint8_t bt = vbt[u];
       const uint8_t xf = vxf[u];
@@ -485,14 +603,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
       if constexpr (kBucket) {
         const bool mito = kCell ? k1_is_mito[k1] != 0 : false;
         const uint64_t kp = make_key(0, k1, k2, hsh, b);
-        keys[p] = payload_w0(kp, ref, rev, mapped, mito);
-        if (ent_hist) {
+        const uint64_t w0 = payload_w0(kp, ref, rev, mapped, mito);
+        const uint64_t w1 = ((uint64_t)p << 32) | (uint32_t)pos;
+        const int sl = slot_of((uint32_t)(e - ebase), lsl);
+        if (sl >= 0) {
           const uint32_t dg = (uint32_t)(kp >> sh1) & ((1u << bits1) - 1u);
-          const int sl = dh_slot(e - ebase);
-          if (sl >= 0) atomicAdd(&s_dh[sl * kRadix + dg], 1u);
-          else atomicAdd(&ent_hist[(size_t)e * kRadix + dg], 1u);
+          const uint32_t dst = atomicAdd(&s_pos[sl * kRadix + dg], 1u);
+          l1.keys_b[dst] = w0;
+          l1.vals_b[dst] = w1;
+        } else {
+          keys[p] = w0;
+          static_cast<uint64_t*>(vals)[p] = w1;
         }
-        static_cast<uint64_t*>(vals)[p] = ((uint64_t)p << 32) | (uint32_t)pos;
         if (mapped && (uint32_t)ref >= (1u << kRefBits)) atomicOr(err, 1u);
       } else {
         keys[p] = make_key((uint64_t)e, k1, k2, hsh, b);
@@ -522,18 +644,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
     }
   }
   wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
-  if constexpr (kBucket) {
-    if (ent_hist) {
-      __syncthreads();
-      for (int i = t; i < kDhRuns * kRadix; i += kBlock) {
-        const uint32_t v = s_dh[i];
-        const int sl = i / kRadix;
-        const int64_t loc = sl < kDhRuns - 1 ? sl : (int64_t)n_heads;  // slot kDhRuns - 1: the last run
-        if (v && (sl < kDhRuns - 1 || n_heads >= (uint32_t)(kDhRuns - 1)))
-          atomicAdd(&ent_hist[(size_t)(ebase + loc) * kRadix + (i % kRadix)], v);
-      }
-    }
-  }
   if (kGene) {
     __syncthreads();
     // the tile's range in each present bucket: its offset inside the bucket (k_gene_emit)

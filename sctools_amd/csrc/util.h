@@ -102,6 +102,7 @@ inline int readback_finish(void* dst, size_t bytes) {
 struct ProfEntry {
   std::string name;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  int64_t items = 0;  // items processed over the timed launches; -1 once a launch did not say
 };
 inline bool& prof_on() {
   static thread_local bool on = false;
@@ -117,11 +118,14 @@ inline std::vector<ProfEntry>& prof_entries() {
   return v;
 }
 
+// items: what the launch processes (records, payloads, sort items), for the algorithmic bytes per
+// launch of the roofline; -1 when the launch does not say
 struct ProfScope {
   hipEvent_t a = nullptr, b = nullptr;
   hipStream_t s;
   const char* name;
-  ProfScope(const char* n, hipStream_t st) : s(st), name(n) {
+  int64_t items;
+  ProfScope(const char* n, hipStream_t st, int64_t it = -1) : s(st), name(n), items(it) {
     if (prof_wants(n) && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
       (void)hipEventRecord(a, s);
   }
@@ -131,9 +135,12 @@ struct ProfScope {
     for (auto& e : prof_entries())
       if (e.name == name) {
         e.ev.emplace_back(a, b);
+        e.items = (e.items < 0 || items < 0) ? -1 : e.items + items;
         return;
       }
-    prof_entries().push_back(ProfEntry{name, {{a, b}}});
+    ProfEntry e{name, {{a, b}}};
+    e.items = items;
+    prof_entries().push_back(e);
   }
 };
 
@@ -144,12 +151,27 @@ struct ProfScope {
   } while (0);                                                   \
   LAUNCHCHK()
 
+// LAUNCH that records the items the launch processes (ProfScope)
+#define LAUNCH_N(name, items, kern, grid, block, strm, ...)      \
+  do {                                                           \
+    ::sct::ProfScope _ps(name, strm, (int64_t)(items));          \
+    hipLaunchKernelGGL(kern, grid, block, 0, strm, __VA_ARGS__); \
+  } while (0);                                                   \
+  LAUNCHCHK()
+
 // with `shm` bytes of dynamic LDS (sct_dyn_lds)
 #define LAUNCH_SHM(name, kern, grid, block, shm, strm, ...)        \
   do {                                                             \
     ::sct::ProfScope _ps(name, strm);                              \
     hipLaunchKernelGGL(kern, grid, block, shm, strm, __VA_ARGS__); \
   } while (0);                                                     \
+  LAUNCHCHK()
+
+#define LAUNCH_SHM_N(name, items, kern, grid, block, shm, strm, ...) \
+  do {                                                               \
+    ::sct::ProfScope _ps(name, strm, (int64_t)(items));              \
+    hipLaunchKernelGGL(kern, grid, block, shm, strm, __VA_ARGS__);   \
+  } while (0);                                                       \
   LAUNCHCHK()
 
 inline int bitlen(uint64_t v) {  // bits for ids 0..v-1; 0 when v <= 1

@@ -2,9 +2,9 @@
 Multi-GPU cell + gene metrics: one process per GPU, cells sharded across ranks.
 
 The reference scales this path by splitting the BAM into cell-disjoint chunks
-(``SplitBam``, ``/root/reference/src/sctools/bam.py:263-410``), running the
+(``SplitBam``, ``/root/reference/src/sctools/bam.py:361-488``), running the
 gatherer on each chunk and merging the CSVs (``MergeCellMetrics`` concatenates,
-``MergeGeneMetrics`` folds, ``metrics/merge.py:66-209``).  Here the same
+``metrics/merge.py:59-71``; ``MergeGeneMetrics`` folds, ``metrics/merge.py:74-191``).  Here the same
 invariant -- no cell spans two shards -- gives:
 
 * cell rows: each rank's rows are final; rank order = record order, so the

@@ -267,12 +267,17 @@ class Engine:
         self.lib.sct_profile_only(kernel.encode())
 
     def profile_read(self) -> Dict[str, Tuple[float, int]]:
+        return {k: v[:2] for k, v in self.profile_read_items().items()}
+
+    def profile_read_items(self) -> Dict[str, Tuple[float, int, int]]:
+        """{kernel: (total ms, launches, items processed over those launches or -1)}; resets."""
         cap = 64
         names = (ctypes.c_char_p * cap)()
         ms = (ctypes.c_double * cap)()
         launches = (ctypes.c_int64 * cap)()
-        k = self.lib.sct_profile_read(names, ms, launches, cap)
-        return {names[i].decode(): (float(ms[i]), int(launches[i])) for i in range(min(k, cap))}
+        items = (ctypes.c_int64 * cap)()
+        k = self.lib.sct_profile_read_items(names, ms, launches, items, cap)
+        return {names[i].decode(): (float(ms[i]), int(launches[i]), int(items[i])) for i in range(min(k, cap))}
 
 
 ORDERS = {"cell": N.ORDER_CELL, "cell_umi_gene": N.ORDER_CELL_UMI_GENE, "gene_cell_umi": N.ORDER_GENE_CELL_UMI}

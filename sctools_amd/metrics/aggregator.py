@@ -5,11 +5,20 @@ reference (``/root/reference/src/sctools/metrics/aggregator.py``:
 533-595), so ``vars(CellMetrics())`` yields the reference CSV header and
 existing callers of the aggregator protocol keep working.
 
-The arithmetic does not live here.  ``parse_molecule`` buffers the records of
-the entity; ``finalize`` columnarizes them and runs the single entity through
-the HIP engine (one launch sequence per entity -- the gatherers batch every
-entity of a file into one launch sequence instead).  The public attributes
-are then filled from the engine's output row.
+``parse_molecule`` keeps the reference's per-record protocol: the plain
+counters (``n_reads``, ``perfect_molecule_barcodes``, ``reads_mapped_*``,
+``duplicate_reads``, ``spliced_reads``, ``perfect_cell_barcodes``,
+``reads_unmapped`` ...) are host integers updated record by record in the
+reference's order, and a missing tag raises its ``KeyError`` (or the empty
+quality string its ``ZeroDivisionError``) inside the ``parse_molecule`` call
+that reads it, after the counters the reference has already updated for that
+record.  Each record's numeric fields are buffered with its tags; ``finalize``
+runs the entity through the HIP engine (one launch sequence per entity -- the
+gatherers batch every entity of a file into one launch sequence instead) for
+the distinct counts and the Welford mean / variance, and fills every public
+attribute from the engine's row.  ``finalize`` of an aggregator that parsed
+nothing gives the reference's values (zero counts, 0.0 means, NaN variances
+and ratios) without a launch.
 """
 
 from typing import Sequence
@@ -17,7 +26,11 @@ from typing import Sequence
 import numpy as np
 
 from sctools_amd import _native as N
+from sctools_amd import columnar as C
+from sctools_amd import consts
 from sctools_amd.metrics import rows as R
+
+_NAN = float("nan")
 
 
 class MetricAggregator:
@@ -55,23 +68,96 @@ class MetricAggregator:
         self.fragments_per_molecule: float = None
         self.fragments_with_single_read_evidence: int = None
         self.molecules_with_single_read_evidence: int = None
-        self._buffered = []
+        self._buffered = []  # (tags, numeric fields) per parsed record
+        self._extra = (0, 0)  # the subclass's CY counts of the record being parsed
 
     # ---- aggregator protocol (aggregator.py:236-340) ----
     def parse_molecule(self, tags: Sequence[str], records) -> None:
+        """aggregator.py:251-334, record by record: the subclass fields first, then the counters,
+        raising where the reference raises."""
         for record in records:
+            self._extra = (0, 0)
             self.parse_extra_fields(tags=tags, record=record)
-            self._buffered.append((tuple(tags), record))
+            cg, cl = self._extra
+            self.n_reads += 1
+            ug, ul = C._frac_counts(record.get_tag(consts.QUALITY_MOLECULE_BARCODE_TAG_KEY))
+            try:
+                self.perfect_molecule_barcodes += record.get_tag(
+                    consts.RAW_MOLECULE_BARCODE_TAG_KEY) == record.get_tag(consts.MOLECULE_BARCODE_TAG_KEY)
+            except KeyError:
+                pass
+            aq = record.query_alignment_qualities
+            if aq is None:
+                raise TypeError("'NoneType' object is not iterable")
+            if len(aq) == 0:
+                raise ZeroDivisionError("division by zero")
+            flag = record.flag
+            b = C.B_PERFECT_UMI if _perfect_umi(record) else 0
+            cb = record.get_tag(consts.CELL_BARCODE_TAG_KEY) if record.has_tag(consts.CELL_BARCODE_TAG_KEY) else None
+            if cb is not None:
+                b |= C.B_HAS_CB
+                if self._MODE == "cell" and record.get_tag(consts.RAW_CELL_BARCODE_TAG_KEY) == cb:
+                    b |= C.B_PERFECT_CB
+            xfv = record.get_tag(consts.ALIGNMENT_LOCATION_TAG_KEY) if record.has_tag(
+                consts.ALIGNMENT_LOCATION_TAG_KEY) else None
+            x = C.XF_ABSENT if xfv is None else C._XF_CODE.get(xfv, C.XF_OTHER)
+            if flag & 0x10:
+                b |= C.B_REVERSE
+            if flag & 0x400:
+                b |= C.B_DUPLICATE
+            if flag & 0x4:
+                b |= C.B_UNMAPPED
+            else:
+                alignment_location = record.get_tag(consts.ALIGNMENT_LOCATION_TAG_KEY)
+                if alignment_location == consts.CODING_ALIGNMENT_LOCATION_TAG_VALUE:
+                    self.reads_mapped_exonic += 1
+                elif alignment_location == consts.INTRONIC_ALIGNMENT_LOCATION_TAG_VALUE:
+                    self.reads_mapped_intronic += 1
+                elif alignment_location == consts.UTR_ALIGNMENT_LOCATION_TAG_VALUE:
+                    self.reads_mapped_utr += 1
+                if record.get_tag(consts.NUMBER_OF_HITS_TAG_KEY) == 1:
+                    self.reads_mapped_uniquely += 1
+                    b |= C.B_NH1
+                else:
+                    self.reads_mapped_multiple += 1
+                if flag & 0x400:
+                    self.duplicate_reads += 1
+                n_len = record.n_skip_length() if hasattr(record, "n_skip_length") else \
+                    record.get_cigar_stats()[0][3]
+                if n_len:
+                    self.spliced_reads += 1
+                    b |= C.B_SPLICED
+                self._plus_strand_reads += not (flag & 0x10)
+            s = sum(aq)
+            if len(aq) > 0xFFFF or s > 0xFFFF or cl > 0xFF or ul > 0xFF:
+                raise ValueError("record %s exceeds the 32-byte columnar limits" % getattr(record, "query_name", "?"))
+            num = (record.reference_id, record.pos, s, len(aq), sum(1 for q in aq if q > 30), b, x, cg, cl, ug, ul)
+            self._buffered.append((tuple(tags), num))
 
     def parse_extra_fields(self, tags: Sequence[str], record) -> None:
-        """Per-record hook; the engine computes the subclass fields at finalize()."""
-        return None
+        """Per-record hook of the subclasses (aggregator.py:336-340)."""
+        raise NotImplementedError
 
     def _run_engine(self, mitochondrial_genes=frozenset(), float_mode="welford"):
         from sctools_amd.metrics.single import aggregate_buffered
 
+        if not self._buffered:
+            self._fill_empty()
+            return
         ints, floats = aggregate_buffered(self._MODE, self._buffered, mitochondrial_genes, float_mode)
         self._fill(ints, floats)
+
+    def _fill_empty(self) -> None:
+        """finalize() with nothing parsed (aggregator.py:350-387): Welford means 0.0 and variances NaN
+        (stats.py:77-100), zero distinct counts, NaN ratios; the counters stay as they are."""
+        for name, kind, _ in R.columns_for(self._MODE):
+            if kind == R.I:
+                if getattr(self, name) is None:
+                    setattr(self, name, 0)
+            elif name.endswith("_mean") or name == "pct_mitochondrial_molecules":
+                setattr(self, name, 0.0)
+            else:
+                setattr(self, name, _NAN)
 
     def _fill(self, ints: np.ndarray, floats: np.ndarray) -> None:
         for name, kind, slot in R.columns_for(self._MODE):
@@ -80,6 +166,13 @@ class MetricAggregator:
 
     def finalize(self) -> None:
         self._run_engine()
+
+
+def _perfect_umi(record) -> bool:
+    try:
+        return record.get_tag(consts.RAW_MOLECULE_BARCODE_TAG_KEY) == record.get_tag(consts.MOLECULE_BARCODE_TAG_KEY)
+    except KeyError:
+        return False
 
 
 class CellMetrics(MetricAggregator):
@@ -102,6 +195,18 @@ class CellMetrics(MetricAggregator):
         self.n_mitochondrial_molecules: int = None
         self.pct_mitochondrial_molecules: float = None
 
+    def parse_extra_fields(self, tags: Sequence[str], record) -> None:
+        """aggregator.py:507-530: CY first, then CB / CR, then XF."""
+        self._extra = C._frac_counts(record.get_tag(consts.QUALITY_CELL_BARCODE_TAG_KEY))
+        if record.has_tag(consts.CELL_BARCODE_TAG_KEY):
+            raw_cell_barcode_tag = record.get_tag(consts.RAW_CELL_BARCODE_TAG_KEY)
+            self.perfect_cell_barcodes += raw_cell_barcode_tag == record.get_tag(consts.CELL_BARCODE_TAG_KEY)
+        try:
+            if record.get_tag(consts.ALIGNMENT_LOCATION_TAG_KEY) == consts.INTERGENIC_ALIGNMENT_LOCATION_TAG_VALUE:
+                self.reads_mapped_intergenic += 1
+        except KeyError:
+            self.reads_unmapped += 1
+
     def finalize(self, mitochondrial_genes=set()):
         self._run_engine(mitochondrial_genes=mitochondrial_genes)
 
@@ -115,6 +220,10 @@ class GeneMetrics(MetricAggregator):
         self._cells_histogram = None
         self.number_cells_detected_multiple: int = None
         self.number_cells_expressing: int = None
+
+    def parse_extra_fields(self, tags: Sequence[str], record) -> None:
+        """aggregator.py:595: the cell tag feeds the distinct cell count at finalize()."""
+        return None
 
     def finalize(self):
         self._run_engine()

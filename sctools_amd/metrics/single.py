@@ -1,7 +1,9 @@
 """
 The aggregator protocol on the engine: ``MetricAggregator.parse_molecule``
-buffers (tags, record) pairs; ``finalize`` turns the buffered entity into
-columns and runs it through the HIP engine as a single-entity batch.
+buffers (tags, numeric fields) pairs -- the fields ``columnar.record_fields``
+would give, read while the counters are updated; ``finalize`` turns the
+buffered entity into columns and runs it through the HIP engine as a
+single-entity batch.
 
 Record semantics follow ``parse_molecule`` / ``parse_extra_fields``
 (``/root/reference/src/sctools/metrics/aggregator.py:236-334, 492-530, 580-595``):
@@ -11,17 +13,16 @@ caller, every other field from the record itself.
 
 import numpy as np
 
-from sctools_amd import columnar, consts
+from sctools_amd import columnar
 
 
 def aggregate_buffered(mode: str, buffered, mitochondrial_genes=frozenset(), float_mode="welford"):
     if not buffered:
-        raise ValueError("finalize() called before any record was parsed")
+        raise ValueError("no buffered records (an empty aggregator finalizes without the engine)")
     is_cell = mode == "cell"
     cell_v, umi_v, gene_v, numeric = [], [], [], []
-    for tags, rec in buffered:
-        cb = rec.get_tag(consts.CELL_BARCODE_TAG_KEY) if rec.has_tag(consts.CELL_BARCODE_TAG_KEY) else None
-        numeric.append(columnar.record_fields(rec, cb, is_cell, True))
+    for tags, num in buffered:
+        numeric.append(num)
         if is_cell:  # tags = (CB, UB, GE)
             cell_v.append(tags[0])
             umi_v.append(tags[1])

@@ -23,7 +23,9 @@ The threads only issue work: H2D copies, C-ABI calls and the collective all rele
 """
 
 import ctypes
+import os
 import threading
+import time
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -33,21 +35,117 @@ from sctools_amd import _native as N
 from sctools_amd import columnar
 from sctools_amd import distributed as D
 
+# bound on the wait for the other ranks at the collective and for its completion (seconds)
+COLLECTIVE_TIMEOUT_S = float(os.environ.get("SCT_COLLECTIVE_TIMEOUT_S", "600"))
+
 
 def parse_devices(devices) -> List[int]:
-    """``devices``: an int N (devices 0..N-1) or a sequence of device indices."""
+    """``devices``: an int N (devices 0..N-1) or a sequence of device indices, one per shard (a
+    device may be listed more than once: several shards on one device)."""
     if isinstance(devices, int):
         if devices < 1:
             raise ValueError("devices must be >= 1")
         return list(range(devices))
     out = [int(d) for d in devices]
-    if not out or len(set(out)) != len(out):
-        raise ValueError("devices must be distinct device indices")
+    if not out or min(out) < 0:
+        raise ValueError("devices must be device indices")
     return out
 
 
+class GroupAborted(RuntimeError):
+    """Raised in a rank whose peers failed: the collective was skipped or cancelled."""
+
+
+class GroupRun:
+    """One call of ``fn(rank)`` on every rank, each in its own thread, with a failure protocol for the
+    one collective of the call (the gene-partial all-reduce):
+
+    * ``before_collective(rank)``: every rank waits here until all ranks arrive (bounded by
+      ``timeout``).  If a rank failed before arriving, the others raise :class:`GroupAborted`
+      instead of issuing a collective whose peers never come;
+    * ``wait(rank, done)``: polls ``done()`` (the collective's completion) until it is true, a rank
+      failed (:class:`GroupAborted`) or the timeout passes (``TimeoutError``);
+    * a failing rank calls ``abort_fn`` once (``ncclCommAbort`` on every communicator), which
+      cancels collectives already in flight on the device.
+
+    ``run`` re-raises the first rank's own error; the :class:`GroupAborted` of its peers only if no
+    rank has another error."""
+
+    def __init__(self, size: int, abort_fn: Optional[Callable[[], None]] = None,
+                 timeout: float = COLLECTIVE_TIMEOUT_S):
+        self.size = size
+        self.timeout = timeout
+        self._abort_fn = abort_fn
+        self._barrier = threading.Barrier(size)
+        self._failed = threading.Event()
+        self._lock = threading.Lock()
+        self.aborted = False
+
+    def fail(self) -> None:
+        with self._lock:
+            if self._failed.is_set():
+                return
+            self._failed.set()
+            self._barrier.abort()
+            if self._abort_fn is not None:
+                self._abort_fn()
+                self.aborted = True
+
+    def before_collective(self, rank: int) -> None:
+        if self._failed.is_set():
+            raise GroupAborted("rank %d: another rank failed before the collective" % rank)
+        try:
+            self._barrier.wait(self.timeout)
+        except threading.BrokenBarrierError:
+            if self._failed.is_set():
+                raise GroupAborted("rank %d: another rank failed before the collective" % rank) from None
+            self.fail()
+            raise TimeoutError("rank %d: the other ranks did not reach the collective within %.0f s"
+                               % (rank, self.timeout)) from None
+
+    def wait(self, rank: int, done: Callable[[], bool]) -> None:
+        deadline = time.monotonic() + self.timeout
+        while not done():
+            if self._failed.is_set():
+                raise GroupAborted("rank %d: another rank failed during the collective" % rank)
+            if time.monotonic() > deadline:
+                self.fail()
+                raise TimeoutError("rank %d: the collective did not complete within %.0f s" % (rank, self.timeout))
+            time.sleep(0.0005)
+
+    def run(self, fn: Callable[[int], object], setup: Optional[Callable[[int], object]] = None) -> List[object]:
+        out: List[object] = [None] * self.size
+        errs: List[Optional[BaseException]] = [None] * self.size
+
+        def work(r):
+            try:
+                if setup is not None:
+                    with setup(r):
+                        out[r] = fn(r)
+                else:
+                    out[r] = fn(r)
+            except BaseException as e:  # re-raised on the caller's thread
+                errs[r] = e
+                self.fail()
+
+        threads = [threading.Thread(target=work, args=(r,)) for r in range(self.size)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        first = next((e for e in errs if e is not None and not isinstance(e, GroupAborted)), None)
+        if first is None:
+            first = next((e for e in errs if e is not None), None)
+        if first is not None:
+            raise first
+        return out
+
+
 class DeviceGroup:
-    """Engines on several devices, one worker thread per device, RCCL communicators on demand."""
+    """Engines on several devices, one worker thread per shard, RCCL communicators on demand.
+
+    Shards listed on one device (``devices=[0, 0]``) share its engine and sum their partials in
+    device memory instead of over RCCL (an RCCL communicator holds one rank per device)."""
 
     def __init__(self, devices):
         from sctools_amd import engine as E
@@ -57,39 +155,33 @@ class DeviceGroup:
             raise RuntimeError("sctools_amd needs ROCm GPUs; there is no CPU fallback")
         if max(self.devices) >= torch.cuda.device_count():
             raise ValueError("device %d requested, %d visible" % (max(self.devices), torch.cuda.device_count()))
-        self.engines = [E.get_engine(torch.device("cuda", d)) for d in self.devices]
+        self.shared = len(set(self.devices)) != len(self.devices)
+        # shards sharing a device get an engine (a workspace) each: their threads run concurrently
+        self.engines = [E.Engine(torch.device("cuda", d)) if self.shared else E.get_engine(torch.device("cuda", d))
+                        for d in self.devices]
         self.lib = N.load()
         self._comms: Optional[ctypes.Array] = None
+        self._run: Optional[GroupRun] = None
+        self._slots: List[Optional[torch.Tensor]] = [None] * len(self.devices)
 
     @property
     def size(self) -> int:
         return len(self.devices)
 
     def run(self, fn: Callable[[int], object]) -> List[object]:
-        """fn(rank) on every rank, each in its own thread with its device current."""
-        out: List[object] = [None] * self.size
-        errs: List[Optional[BaseException]] = [None] * self.size
+        """fn(rank) on every rank, each in its own thread with its device current.  If a rank raises,
+        the group's collective is skipped (or aborted) on every rank and the error is re-raised here."""
+        self._run = GroupRun(self.size, abort_fn=self.abort)
+        try:
+            return self._run.run(fn, setup=lambda r: torch.cuda.device(self.devices[r]))
+        finally:
+            self._run = None
 
-        def work(r):
-            try:
-                with torch.cuda.device(self.devices[r]):
-                    out[r] = fn(r)
-            except BaseException as e:  # re-raised on the caller's thread
-                errs[r] = e
-
-        threads = [threading.Thread(target=work, args=(r,)) for r in range(self.size)]
-        for t in threads:
-            t.start()
-        for t in threads:
-            t.join()
-        for e in errs:
-            if e is not None:
-                raise e
-        return out
-
-    def comms(self) -> ctypes.Array:
-        """The group's communicators (ncclCommInitAll); create them on the caller's thread before
-        the ranks' threads use them."""
+    def comms(self) -> Optional[ctypes.Array]:
+        """The group's communicators (ncclCommInitAll; none for shards sharing a device); create them
+        on the caller's thread before the ranks' threads use them."""
+        if self.shared:
+            return None
         if self._comms is None:
             comms = (ctypes.c_void_p * self.size)()
             devs = (ctypes.c_int * self.size)(*self.devices)
@@ -98,12 +190,50 @@ class DeviceGroup:
         return self._comms
 
     def allreduce_partials(self, rank: int, partials: torch.Tensor) -> None:
-        """In-place sum of every rank's [rows, SCT_NP] int64 partials (call from every rank's thread)."""
+        """In-place sum of every rank's [rows, SCT_NP] int64 partials (call from every rank's thread,
+        inside run()).  Returns once the sum is complete on this rank's stream."""
         if partials.dtype != torch.int64 or not partials.is_contiguous():
             raise TypeError("partials must be contiguous int64")
-        stream = ctypes.c_void_p(torch.cuda.current_stream(partials.device).cuda_stream)
+        g = self._run
+        if g is None:
+            raise RuntimeError("allreduce_partials is called from the ranks of DeviceGroup.run")
+        g.before_collective(rank)
+        stream = torch.cuda.current_stream(partials.device)
+        if self.shared:
+            self._local_sum(rank, partials)
+            return
         N.check(self.lib.sct_allreduce_gene_partials(ctypes.c_void_p(partials.data_ptr()), int(partials.shape[0]),
-                                                     ctypes.c_void_p(self.comms()[rank]), stream))
+                                                     ctypes.c_void_p(self.comms()[rank]),
+                                                     ctypes.c_void_p(stream.cuda_stream)))
+        done = torch.cuda.Event()
+        done.record(stream)
+        g.wait(rank, done.query)
+
+    def _local_sum(self, rank: int, partials: torch.Tensor) -> None:
+        """Shards on shared devices: every rank's partials become the sum of all (device memory)."""
+        g = self._run
+        torch.cuda.current_stream(partials.device).synchronize()
+        self._slots[rank] = partials
+        g.before_collective(rank)  # every slot filled
+        if rank == 0:
+            tot = self._slots[0].clone()
+            for t in self._slots[1:]:
+                tot += t.to(tot.device)
+            torch.cuda.current_stream(tot.device).synchronize()
+            self._slots = [tot] + [None] * (self.size - 1)
+        g.before_collective(rank)  # the sum is ready
+        partials.copy_(self._slots[0].to(partials.device))
+        torch.cuda.current_stream(partials.device).synchronize()
+        g.before_collective(rank)  # every rank has copied it
+        if rank == 0:
+            self._slots = [None] * self.size
+
+    def abort(self) -> None:
+        """A rank failed: cancel the collective on every communicator (ncclCommAbort)."""
+        if self._comms is not None:
+            comms, self._comms = self._comms, None
+            for c in comms:
+                self.lib.sct_comm_abort(ctypes.c_void_p(c))
 
     def close(self) -> None:
         if self._comms is not None:

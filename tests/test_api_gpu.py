@@ -192,3 +192,89 @@ def test_allreduce_c_abi_with_own_communicator():
         assert lib.sct_allreduce_gene_partials(None, 5, comm, s) == -1
     finally:
         N.check(lib.sct_comm_destroy(comm))
+
+
+def test_aggregator_protocol_golden_finalize():
+    """The protocol golden's undamaged (and damaged-but-not-raising) cases finalized on the GPU:
+    every public attribute equals the reference aggregator's (tests/golden/protocol)."""
+    import math
+
+    import test_protocol_cpu as P
+
+    done = 0
+    for case in P.CASES:
+        if case["final"] is None:
+            continue
+        agg, _, raised = P.replay(case)
+        assert raised is None
+        agg.finalize()
+        got = {k: v for k, v in vars(agg).items() if not k.startswith("_")}
+        assert list(got) == list(case["final"])
+        for k, v in got.items():
+            w = case["final"][k]
+            if w == "nan":
+                assert isinstance(v, float) and math.isnan(v), (case["entity_name"], k)
+            else:
+                assert str(v) == w, (case["entity_name"], case["damage"], k, v, w)
+        done += 1
+    assert done >= 8
+
+
+@pytest.mark.parametrize("bam", H.BAMS)
+@pytest.mark.parametrize("kind", ["cell", "gene"])
+def test_gatherers_three_shards_on_one_device(tmp_path, bam, kind):
+    """devices=[0, 0, 0]: the file cut into three entity-aligned shards (record offsets > 0), each
+    on its own thread and engine of device 0, rows concatenated: the reference's CSV byte for byte."""
+    from sctools_amd.metrics import GatherCellMetrics, GatherGeneMetrics
+
+    cls = GatherCellMetrics if kind == "cell" else GatherGeneMetrics
+    stem = str(tmp_path / "out")
+    cls(os.path.join(BAM_DIR, bam + ".bam"), stem, compress=False, devices=[0, 0, 0]).extract_metrics()
+    assert _read(stem + ".csv") == H.golden_text(bam, kind)
+
+
+@pytest.mark.parametrize("float_mode", ["exact", "welford"])
+def test_shards_with_an_empty_shard_equal_one_device(float_mode):
+    """A record set whose first cell holds most records: three shards cut at cell boundaries leave
+    the middle one empty (zero partials, no rows).  Cell rows, first-record offsets and the summed
+    gene partials equal the one-device result exactly."""
+    import numpy as np
+
+    from sctools_amd import columnar, distributed as D, multigpu
+
+    full = columnar.columnarize(os.path.join(BAM_DIR, "cell-sorted-missing-cb.bam"), "rb", "cell")
+    cols = columnar.Columns({c: a[:216] for c, a in full.arrays.items()}, full.cells, full.umis, full.genes)
+    bounds = D.shard_bounds(cols.arrays["cell"], 3)
+    assert any(lo == hi for lo, hi in bounds), bounds
+    one = multigpu.compute_cell_and_gene_rows(cols, float_mode=float_mode, devices=[0])
+    three = multigpu.compute_cell_and_gene_rows(cols, float_mode=float_mode, devices=[0, 0, 0])
+    for a, b in zip(one[0] + one[1], three[0] + three[1]):
+        assert np.array_equal(np.nan_to_num(a, nan=-7.0), np.nan_to_num(b, nan=-7.0))
+    r1 = multigpu.compute_rows(cols, "cell", float_mode=float_mode, devices=[0])
+    r3 = multigpu.compute_rows(cols, "cell", float_mode=float_mode, devices=[0, 0, 0])
+    for a, b in zip(r1, r3):
+        assert np.array_equal(np.nan_to_num(a, nan=-7.0), np.nan_to_num(b, nan=-7.0))
+
+
+def test_shard_failure_raises_without_hanging(monkeypatch):
+    """One shard's engine call fails (injected) while the others wait at the gene-partial collective:
+    the group raises that error promptly instead of blocking in the all-reduce."""
+    import time
+
+    from sctools_amd import columnar, engine as E, multigpu
+
+    cols = columnar.columnarize(os.path.join(BAM_DIR, "small-cell-sorted.bam"), "rb", "cell")
+    real = E.Engine.cell_and_gene
+    calls = []
+
+    def flaky(self, *a, **k):
+        calls.append(1)
+        if len(calls) == 2:
+            raise MemoryError("injected: shard engine out of memory")
+        return real(self, *a, **k)
+
+    monkeypatch.setattr(E.Engine, "cell_and_gene", flaky)
+    t0 = time.monotonic()
+    with pytest.raises(MemoryError, match="injected"):
+        multigpu.compute_cell_and_gene_rows(cols, float_mode="exact", devices=[0, 0, 0])
+    assert time.monotonic() - t0 < 60
