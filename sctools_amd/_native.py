@@ -154,8 +154,9 @@ def load() -> ctypes.CDLL:
     L.sct_comm_init_all.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.sct_comm_destroy.restype = ctypes.c_int
     L.sct_comm_destroy.argtypes = [vp]
-    L.sct_comm_abort.restype = ctypes.c_int
-    L.sct_comm_abort.argtypes = [vp]
+    if hasattr(L, "sct_comm_abort"):
+        L.sct_comm_abort.restype = ctypes.c_int
+        L.sct_comm_abort.argtypes = [vp]
     L.sct_profile_enable.restype = ctypes.c_int
     L.sct_profile_enable.argtypes = [ctypes.c_int]
     L.sct_profile_only.restype = ctypes.c_int
@@ -163,9 +164,11 @@ def load() -> ctypes.CDLL:
     L.sct_profile_read.restype = ctypes.c_int
     L.sct_profile_read.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(i64), ctypes.c_int]
-    L.sct_profile_read_items.restype = ctypes.c_int
-    L.sct_profile_read_items.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
-                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+    if hasattr(L, "sct_profile_read_items"):  # (an older engine given by SCT_LIB_PATH for an A/B lacks it)
+        L.sct_profile_read_items.restype = ctypes.c_int
+        L.sct_profile_read_items.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                             ctypes.c_int]
     if L.sct_abi_version() != SCT_ABI_VERSION:
         raise ImportError("libsctools_gpu.so ABI %d != %d" % (L.sct_abi_version(), SCT_ABI_VERSION))
     _lib = L

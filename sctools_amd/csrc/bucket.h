@@ -25,7 +25,8 @@
 // molecule has > kBCap records) carries flags so exactly one piece counts its head and the
 // group's ">= 2 records" event.
 //
-// Records travel as a 16-byte payload (two u64 words, SoA) so no pass gathers by index:
+// Records travel as a 16-byte payload (Pay: two u64 words side by side, one 16-byte load or store
+// per record) so no pass gathers by index:
 //   w0 = key' << 17 | ref (14 bits) << 3 | strand << 2 | mapped << 1 | k1 is mitochondrial
 //   w1 = record index << 32 | pos (uint32)
 // key' = [k1' | k2 | hash] with k1' = k1 * odd mod 2^k1 (Bits::scramble), so heavy genes with
@@ -88,6 +89,12 @@ enum : uint16_t {
 struct Seg {
   uint32_t start, cnt, ent, flags;
 };
+struct alignas(16) Pay {
+  uint64_t w0, w1;
+};
+__device__ __forceinline__ uint64_t pay_w0(const Pay* p, size_t i) {  // w0 alone: an 8-byte load
+  return reinterpret_cast<const uint64_t*>(p)[2 * i];
+}
 struct alignas(16) Work {  // one chunk of a segment: its records [beg, beg + n), n <= kChunk
   uint32_t seg, beg, n, pad;
 };
@@ -146,7 +153,7 @@ __global__ void k_bucket_level0(const int64_t* __restrict__ ent_start, int64_t n
   push_segment(Seg{(uint32_t)s0, c, (uint32_t)e, 0u}, seg, work, seg_ctr);
 }
 
-__global__ void __launch_bounds__(kBlock) k_bucket_hist(const uint64_t* __restrict__ keys, const Seg* __restrict__ seg,
+__global__ void __launch_bounds__(kBlock) k_bucket_hist(const Pay* __restrict__ pin, const Seg* __restrict__ seg,
                                                         const Work* __restrict__ work, int shift, int bits,
                                                         uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[kWaves][kRadix];
@@ -157,7 +164,7 @@ __global__ void __launch_bounds__(kBlock) k_bucket_hist(const uint64_t* __restri
   const uint32_t end = wk.beg + wk.n;
   const uint64_t mask = (1ull << bits) - 1;
   __syncthreads();
-  for (uint32_t p = beg + threadIdx.x; p < end; p += kBlock) atomicAdd(&h[wid][(keys[p] >> shift) & mask], 1u);
+  for (uint32_t p = beg + threadIdx.x; p < end; p += kBlock) atomicAdd(&h[wid][(pay_w0(pin, p) >> shift) & mask], 1u);
   __syncthreads();
   const int d = threadIdx.x;
   uint32_t tot = 0;
@@ -215,13 +222,10 @@ __device__ __forceinline__ uint32_t digit_starts(uint32_t (*whist)[kRadix], uint
 constexpr int kSBlock = 512;
 constexpr int kSItems = kChunk / kSBlock;
 static_assert(kRadix <= kSBlock, "one thread per digit");
-__global__ void __launch_bounds__(kSBlock) k_bucket_scatter(const uint64_t* __restrict__ kin,
-                                                            const uint64_t* __restrict__ vin,
-                                                            uint64_t* __restrict__ kout, uint64_t* __restrict__ vout,
+__global__ void __launch_bounds__(kSBlock) k_bucket_scatter(const Pay* __restrict__ pin, Pay* __restrict__ pout,
                                                             const Seg* __restrict__ seg, const Work* __restrict__ work,
                                                             int shift, int bits, uint32_t* __restrict__ cur) {
-  __shared__ uint64_t s_keys[kChunk];
-  __shared__ uint64_t s_vals[kChunk];
+  __shared__ Pay s_pay[kChunk];
   __shared__ uint32_t s_cnt[kRadix];
   __shared__ uint32_t s_start[kRadix];
   __shared__ uint32_t s_gbase[kRadix];
@@ -233,21 +237,17 @@ __global__ void __launch_bounds__(kSBlock) k_bucket_scatter(const uint64_t* __re
   const uint32_t mask = (1u << bits) - 1;
   if (t < kRadix) s_cnt[t] = 0;
   __syncthreads();
-  uint64_t k[kSItems];
-  uint64_t v[kSItems];
+  Pay k[kSItems];
   uint32_t rk[kSItems];
 #pragma unroll
   for (int j = 0; j < kSItems; j++) {
     const int q = j * kSBlock + t;
-    if (q < tile_n) {
-      k[j] = kin[beg + q];
-      v[j] = vin[beg + q];
-    }
+    if (q < tile_n) k[j] = pin[beg + q];
   }
 #pragma unroll
   for (int j = 0; j < kSItems; j++) {
     const int q = j * kSBlock + t;
-    if (q < tile_n) rk[j] = atomicAdd(&s_cnt[(uint32_t)(k[j] >> shift) & mask], 1u);
+    if (q < tile_n) rk[j] = atomicAdd(&s_cnt[(uint32_t)(k[j].w0 >> shift) & mask], 1u);
   }
   __syncthreads();
   {
@@ -263,19 +263,13 @@ __global__ void __launch_bounds__(kSBlock) k_bucket_scatter(const uint64_t* __re
 #pragma unroll
   for (int j = 0; j < kSItems; j++) {
     const int q = j * kSBlock + t;
-    if (q < tile_n) {
-      const uint32_t lp = s_start[(uint32_t)(k[j] >> shift) & mask] + rk[j];
-      s_keys[lp] = k[j];
-      s_vals[lp] = v[j];
-    }
+    if (q < tile_n) s_pay[s_start[(uint32_t)(k[j].w0 >> shift) & mask] + rk[j]] = k[j];
   }
   __syncthreads();
   for (int q = t; q < tile_n; q += kSBlock) {
-    const uint64_t kk = s_keys[q];
-    const uint32_t d = (uint32_t)(kk >> shift) & mask;
-    const uint32_t o = s_gbase[d] + (uint32_t)(q - (int)s_start[d]);
-    kout[o] = kk;
-    vout[o] = s_vals[q];
+    const Pay kk = s_pay[q];
+    const uint32_t d = (uint32_t)(kk.w0 >> shift) & mask;
+    pout[s_gbase[d] + (uint32_t)(q - (int)s_start[d])] = kk;
   }
 }
 
@@ -365,13 +359,11 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
   const uint64_t sw = block_exclusive_scan<uint64_t>(((uint64_t)(push ? 1 : 0) << 32) | nw, &tot_sw, s_scan);
   const uint32_t so = (uint32_t)(sw >> 32), wo = (uint32_t)sw;
   const uint64_t tot_s = tot_sw >> 32, tot_w = tot_sw & 0xffffffffull;
-  uint64_t tot_r;  // the new segments' records
-  (void)block_exclusive_scan<uint64_t>(push ? c : 0u, &tot_r, s_scan);
   if (d == 0 && tot_s) {
     s_base[0] = atomicAdd(&ctl->n_seg, (uint32_t)tot_s);
     s_base[1] = atomicAdd(&ctl->n_work, (uint32_t)tot_w);
-    atomicAdd(&ctl->n_rec, (uint32_t)tot_r);
   }
+  if (push) atomicAdd(&ctl->n_rec, c);  // the new segments' records (a few per block)
   __syncthreads();
   if (push) {
     const uint32_t id = s_base[0] + so;
@@ -438,10 +430,8 @@ __device__ __forceinline__ uint32_t ht_insert_cap(E* T, E key, int& ev) {
 template <bool kCell, bool kGene, bool kWideK1>
 __global__ void __launch_bounds__(kHBlock) k_hash_tile(const uint16_t* __restrict__ bdesc,
                                                        const uint32_t* __restrict__ bent,
-                                                       const uint64_t* __restrict__ w0_a,
-                                                       const uint64_t* __restrict__ w1_a,
-                                                       const uint64_t* __restrict__ w0_b,
-                                                       const uint64_t* __restrict__ w1_b, int64_t n, Bits b,
+                                                       const Pay* __restrict__ pay_a,
+                                                       const Pay* __restrict__ pay_b, int64_t n, Bits b,
                                                        int64_t* __restrict__ partials,
                                                        uint16_t* __restrict__ dflags) {
   using K1E = typename std::conditional<kWideK1, unsigned long long, unsigned int>::type;
@@ -530,9 +520,8 @@ __global__ void __launch_bounds__(kHBlock) k_hash_tile(const uint16_t* __restric
     wave_flush<kDistinct>(acc, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
     if (!valid) continue;
     cur_e = e;
-    const bool pb = bd & BD_PARITY;
-    const uint64_t x0 = pb ? w0_b[w0 + q] : w0_a[w0 + q];
-    const uint64_t x1 = pb ? w1_b[w0 + q] : w1_a[w0 + q];
+    const Pay x = ((bd & BD_PARITY) ? pay_b : pay_a)[w0 + q];
+    const uint64_t x0 = x.w0, x1 = x.w1;
     const uint64_t key = (x0 >> kKeyShift) & kmask;  // ids >= the dictionary sizes stay inside KB bits
     int ek = 0, em, ef = 0;
     const uint32_t ms =
@@ -570,10 +559,8 @@ __global__ void __launch_bounds__(kHBlock) k_hash_tile(const uint16_t* __restric
 // per-record logic with one bucket per block and kBigSlots-slot tables.
 template <bool kCell, bool kGene, bool kWideK1>
 __global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict__ bigs,
-                                                          const uint64_t* __restrict__ w0_a,
-                                                          const uint64_t* __restrict__ w1_a,
-                                                          const uint64_t* __restrict__ w0_b,
-                                                          const uint64_t* __restrict__ w1_b, Bits b,
+                                                          const Pay* __restrict__ pay_a,
+                                                          const Pay* __restrict__ pay_b, Bits b,
                                                           int64_t* __restrict__ partials,
                                                           uint16_t* __restrict__ dflags) {
   using K1E = typename std::conditional<kWideK1, unsigned long long, unsigned int>::type;
@@ -595,9 +582,7 @@ __global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict_
   }
   __syncthreads();
   const uint32_t bd = g.flags;
-  const bool pb = bd & BD_PARITY;
-  const uint64_t* W0 = pb ? w0_b : w0_a;
-  const uint64_t* W1 = pb ? w1_b : w1_a;
+  const Pay* P = (bd & BD_PARITY) ? pay_b : pay_a;
   const int KB = b.k1 + b.k2 + b.h;
   const uint64_t kmask = (1ull << KB) - 1;
   const int sh_mol = b.h, sh_k1 = b.k2 + b.h;
@@ -605,8 +590,8 @@ __global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict_
 #pragma unroll
   for (int i = 0; i < kDistinct; i++) acc[i] = 0;
   for (uint32_t p = t; p < g.cnt; p += kBigBlock) {
-    const uint64_t x0 = W0[g.start + p];
-    const uint64_t x1 = W1[g.start + p];
+    const Pay x = P[g.start + p];
+    const uint64_t x0 = x.w0, x1 = x.w1;
     const uint64_t key = (x0 >> kKeyShift) & kmask;
     int ek = 0, em, ef = 0;
     const uint32_t ms = ht_insert<unsigned long long>(s_mol, (key >> sh_mol) << 2, em, tb);
@@ -650,22 +635,29 @@ __global__ void __launch_bounds__(kBigBlock) k_big_bucket(const Seg* __restrict_
 // A bucket whose whole key' is fixed and still holds > kBCap records: one piece of one
 // molecule at one fragment hash.  One block; fragments resolved exactly by repeatedly taking
 // the first unassigned mapped record as a representative.  `mark` is the other buffer's w1
-// array over the same range (dead: the parent segment was scattered out of it).
+// words over the same range (dead: the parent segment was scattered out of it).
 template <bool kCell, bool kGene>
-__global__ void __launch_bounds__(kBlock) k_bucket_giant(const Seg* __restrict__ giants,
-                                                         const uint64_t* __restrict__ w0_a,
-                                                         uint64_t* __restrict__ w1_a,
-                                                         const uint64_t* __restrict__ w0_b,
-                                                         uint64_t* __restrict__ w1_b,
-                                                         int64_t* __restrict__ partials,
+__global__ void __launch_bounds__(kBlock) k_bucket_giant(const Seg* __restrict__ giants, Pay* __restrict__ pay_a,
+                                                         Pay* __restrict__ pay_b, int64_t* __restrict__ partials,
                                                          uint16_t* __restrict__ dflags) {
   __shared__ uint64_t s_red[kWaves];
   __shared__ uint32_t s_min[kWaves];
   const Seg g = giants[blockIdx.x];
   const bool pb = g.flags & BD_PARITY;
-  const uint64_t* w0 = pb ? w0_b : w0_a;
-  const uint64_t* w1 = pb ? w1_b : w1_a;
-  uint64_t* mark = pb ? w1_a : w1_b;
+  const Pay* P = pb ? pay_b : pay_a;
+  Pay* other = pb ? pay_a : pay_b;
+  struct W0 {
+    const Pay* p;
+    __device__ uint64_t operator[](size_t i) const { return p[i].w0; }
+  } w0{P};
+  struct W1 {
+    const Pay* p;
+    __device__ uint64_t operator[](size_t i) const { return p[i].w1; }
+  } w1{P};
+  struct Mark {
+    Pay* p;
+    __device__ uint64_t& operator[](size_t i) const { return p[i].w1; }
+  } mark{other};
   const int t = threadIdx.x;
   const int lane = t & (kWave - 1);
   const int wid = t / kWave;

@@ -84,13 +84,15 @@ struct Welford {
 // update depends on record k-1's rounded mean, so an entity's chain cannot be split.  What can
 // run in parallel is everything off the chain, and entities run side by side:
 //   * entities of < kWfWave records: one lane each (k_welford);
-//   * larger ones: one wave each (k_welford_wave), largest first (k_welford_bins / _order put
-//     them in descending log2-size order, waves dequeue them): per chunk of 64 records all 64
-//     lanes load the columns (coalesced) and compute the stream values x = RN(a / b) and
-//     y = RN(1 / k) in parallel; then one lane per stream runs the chain over the chunk from LDS.
-//     The chain's division delta / k is RN(q0 + r y) with q0 = RN(delta y), r = fma(-q0, k, delta)
-//     (exact), the correctly rounded quotient for y = RN(1/k) (Markstein; tests/native/welfdiv.c
-//     checks it against IEEE division), so each update is bit-identical to Python's.
+//   * larger ones: one lane per (entity, stream) chain (k_welford_chains), largest first
+//     (k_welford_bins / _order put them in descending log2-size order, waves dequeue groups of
+//     them), over the stream values x = RN(a / b) computed once for every record (k_welford_x).
+//     The chain's division delta / k uses a double-double reciprocal 1/k ~ y_hi + y_lo
+//     (y_hi = RN(1/k), y_lo = RN(fma(-k, y_hi, 1) y_hi)): q = fma(delta, y_hi, RN(delta y_lo)) is
+//     within 2^-104 of delta / k, which is never that close to a rounding midpoint unless it is a
+//     double, so q = RN(delta / k) (tests/native/welfdiv.c checks it against IEEE division) and
+//     each update is bit-identical to Python's.  The longest entity's chain bounds the time: 4
+//     dependent FP64 operations per record (sub, mul, fma, add), no memory or LDS latency on it.
 constexpr int kWfWave = 48;  // records from which an entity gets a wave of its own
 constexpr int kWfBins = 32;  // log2 size classes
 struct WelfordCtl {
@@ -153,67 +155,114 @@ __device__ __forceinline__ void welford_store(double* F, int st, double mean, do
   F[vslot] = var;
 }
 
-// Persistent: each wave dequeues big entities (largest first) until the queue is empty.
-constexpr int kWfBlocks = 2048;
+// The stream values of every record, once, in parallel: xs[st * n + i] = x[st] of record i
+// (welford_samples); the chains below then load one double per record.
 template <bool kCell>
-__global__ void __launch_bounds__(kBlock) k_welford_wave(RecCols r, const int64_t* __restrict__ ent_start,
-                                                         int64_t n_ent, int64_t n, const uint32_t* __restrict__ order,
-                                                         WelfordCtl* __restrict__ ctl, double* __restrict__ out_f) {
-  constexpr int ns = kCell ? 4 : 3;
-  __shared__ double s_x[kWaves][4][kWave + 2];  // +2: the 4 chain lanes read 4 different banks
-  __shared__ double s_y[kWaves][kWave];
+__global__ void __launch_bounds__(kBlock) k_welford_x(RecCols r, int64_t n, double* __restrict__ xs) {
   __shared__ double s_rcp[kRcpN];
   fill_rcp(s_rcp);
   __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  double x[4];
+  welford_samples<kCell>(r, i, s_rcp, x);
+#pragma unroll
+  for (int st = 0; st < (kCell ? 4 : 3); st++) xs[st * n + i] = x[st];
+}
+
+// Big entities: one lane per (entity, stream) chain, kWfGroup entities x 4 streams per wave, groups
+// of similar sizes (the order is by descending log2 size), waves dequeue groups.  Every lane steps
+// the same record index k together, so RN(1 / k) is the same for all of them: the wave computes 64
+// of them at a time into LDS (one division per lane per 64 records).  Per record a lane loads its
+// sample (kWfBatch records per batch; the next batch's loads, unconditional with clamped addresses,
+// are in flight while this batch's kWfBatch updates run: enough work to cover HBM latency) and runs
+// the update: the chain is 5 dependent FP64 operations, and nothing on it waits for memory.
+constexpr int kWfGroup = kWave / 4;
+constexpr int kWfBatch = 32;
+static_assert(kWave % kWfBatch == 0, "batches tile the 64-record y chunks");
+constexpr int kWfBlocks = 2048;  // persistent grid (waves dequeue groups)
+template <bool kCell>
+__global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __restrict__ ent_start, int64_t n_ent,
+                                                           int64_t n, const uint32_t* __restrict__ order,
+                                                           WelfordCtl* __restrict__ ctl,
+                                                           const double* __restrict__ xs, double* __restrict__ out_f) {
+  constexpr int ns = kCell ? 4 : 3;
+  __shared__ double s_yh[kWaves][kWave];
+  __shared__ double s_yl[kWaves][kWave];
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = threadIdx.x / kWave;
+  const int st = lane & 3;
   const uint32_t n_big = ctl->n_big;
+  const uint32_t n_groups = (n_big + kWfGroup - 1) / kWfGroup;
   while (true) {
-    uint32_t k = 0;
-    if (lane == 0) k = atomicAdd(&ctl->head, 1u);
-    k = (uint32_t)__shfl((int)k, 0);
-    if (k >= n_big) break;  // wave-uniform: every wave reaches it once the queue is drained
-    const int64_t e = order[k];
-    const int64_t s = ent_start[e];
-    const int64_t t = ent_end(ent_start, e, n_ent, n);
-    double mean = 0.0, m2 = 0.0, cnt = 0.0;
-    double x[4], xn[4];
-    if (s + lane < t) welford_samples<kCell>(r, s + lane, s_rcp, x);
-    for (int64_t c = s; c < t; c += kWave) {
-      // this chunk's samples and reciprocals to LDS; the next chunk's loads go out meanwhile
-      const int64_t j = c + lane;
+    uint32_t g = 0;
+    if (lane == 0) g = atomicAdd(&ctl->head, 1u);
+    g = (uint32_t)__shfl((int)g, 0);
+    if (g >= n_groups) break;  // wave-uniform: every wave reaches it once the queue is drained
+    const uint32_t k = g * kWfGroup + (uint32_t)(lane >> 2);
+    const bool mine = k < n_big && st < ns;
+    int64_t e = 0, s = 0, len = 0;
+    if (mine) {
+      e = order[k];
+      s = ent_start[e];
+      len = ent_end(ent_start, e, n_ent, n) - s;
+    }
+    int64_t kmax = len;  // the wave's longest chain
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+      const int64_t o = __shfl_xor(kmax, off);
+      kmax = o > kmax ? o : kmax;
+    }
+    const double* X = xs + (int64_t)st * n + s;  // (a lane without a chain reads xs[st n], never used)
+    const int64_t lastx = len > 0 ? len - 1 : 0;
+    double mean = 0.0, m2 = 0.0;
+    double xb[kWfBatch], xn[kWfBatch];
 #pragma unroll
-      for (int st = 0; st < 4; st++) s_x[wv][st][lane] = x[st];
-      s_y[wv][lane] = 1.0 / (double)(j - s + 1);
-      if (c + kWave + lane < t) welford_samples<kCell>(r, c + kWave + lane, s_rcp, xn);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int m = (int)((t - c) < kWave ? (t - c) : kWave);
-      if (lane < ns) {
-        for (int q = 0; q < m; q++) {
-          const double xv = s_x[wv][lane][q];
-          const double y = s_y[wv][q];
-          cnt += 1.0;
-          const double delta = xv - mean;
-          const double q0 = delta * y;
-          const double rr = __fma_rn(-q0, cnt, delta);
-          mean = mean + __fma_rn(rr, y, q0);  // == mean + delta / cnt
-          const double delta2 = xv - mean;
-          m2 = m2 + delta * delta2;
-        }
+    for (int q = 0; q < kWfBatch; q++) xb[q] = X[q < lastx ? q : lastx];
+    for (int64_t c0 = 0; c0 < kmax; c0 += kWave) {
+      {  // 1 / k for this chunk's 64 record indices, as y_hi + y_lo
+        const double k = (double)(c0 + lane + 1);
+        const double yh = 1.0 / k;
+        s_yh[wv][lane] = yh;
+        s_yl[wv][lane] = __fma_rn(-k, yh, 1.0) * yh;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int64_t c1 = c0 + kWave < kmax ? c0 + kWave : kmax;
+      for (int64_t c = c0; c < c1; c += kWfBatch) {
 #pragma unroll
-      for (int st = 0; st < 4; st++) x[st] = xn[st];
+        for (int q = 0; q < kWfBatch; q++) {
+          const int64_t kq = c + kWfBatch + q;
+          xn[q] = X[kq < lastx ? kq : lastx];
+        }
+        const auto update = [&](int q) {
+          const double delta = xb[q] - mean;
+          mean = mean + __fma_rn(delta, s_yh[wv][c - c0 + q], delta * s_yl[wv][c - c0 + q]);  // + RN(delta / k)
+          const double delta2 = xb[q] - mean;
+          m2 = m2 + delta * delta2;
+        };
+        if (c + kWfBatch <= len) {
+#pragma unroll
+          for (int q = 0; q < kWfBatch; q++) update(q);
+        } else {
+#pragma unroll
+          for (int q = 0; q < kWfBatch; q++)
+            if (c + q < len) update(q);
+        }
+#pragma unroll
+        for (int q = 0; q < kWfBatch; q++) xb[q] = xn[q];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // s_y is rewritten by the next chunk
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    double* F = out_f + e * SCT_NF;
-    if (lane < ns) welford_store<kCell>(F, lane, mean, m2, t - s);
-    if (!kCell && lane == 0) {
-      F[SCT_F_CY_MEAN] = 0.0;
-      F[SCT_F_CY_VAR] = 0.0;
+    if (mine) {
+      double* F = out_f + e * SCT_NF;
+      welford_store<kCell>(F, st, mean, m2, len);
+      if (!kCell && st == 0) {
+        F[SCT_F_CY_MEAN] = 0.0;
+        F[SCT_F_CY_VAR] = 0.0;
+      }
     }
   }
 }

@@ -22,7 +22,9 @@
 
 namespace sct {
 
-constexpr int kGeneChunk = 16384;  // payloads per reduce block
+// payloads per reduce work item (each item ends with up to kGenesPerBucket x 39 global atomics into
+// the gene rows; 65536-payload items measured 0.87-0.89 ms against 0.85 at config 2)
+constexpr int kGeneChunk = 16384;
 constexpr int kGeneSub = 2048;  // 16-byte payloads sorted in LDS at a time (32 KB)
 constexpr int kGeneCnt = 1 + kGeneFlags;  // n_reads + flag counts (32-bit bins)
 constexpr int kGeneCntPad = 16;
@@ -314,8 +316,8 @@ __device__ __forceinline__ void fill_uy_tab(uint32_t B, uint4* tab) {
 }
 
 // A thread's open run of one gene.  The 16 counted flag bits are counted in bytes of pk (a run
-// stays open over the sub-tiles of one work item: at most kGeneChunk / kSub * kItems payloads),
-// two 64-bit adds per payload instead of one extract-and-add per flag.
+// stays open over the sub-tiles of one work item, and is flushed before it could reach
+// kRunCap payloads), two 64-bit adds per payload instead of one extract-and-add per flag.
 struct GeneAcc {
   uint64_t pk[2];  // byte f of pk[f / 8]: #payloads with counted bit f
   int32_t n;       // n_reads
@@ -355,8 +357,9 @@ struct GeneAcc {
     for (int i = 0; i < 3 * kStreamLanes; i++) atomicAdd(&lbin[i], (unsigned long long)l[i]);
   }
 };
-static_assert(kGeneChunk / GeneFmt<false>::kSub * (GeneFmt<false>::kSub / kBlock) <= 255, "byte counters");
-static_assert(kGeneChunk / GeneFmt<true>::kSub * (GeneFmt<true>::kSub / kBlock) <= 255, "byte counters");
+constexpr int kRunCap = 255;  // byte counters
+static_assert(GeneFmt<false>::kSub / kBlock <= kRunCap / 2 && GeneFmt<true>::kSub / kBlock <= kRunCap / 2,
+              "a sub-tile adds at most kItems payloads to an open run");
 
 // Segmented inclusive DPP scan over the wave: lanes hold partial sums of the segment (adjacent
 // lanes with equal keys) that starts at lane `seg`.  Step j adds the value of the lane 1, 2, 4, 8
@@ -499,8 +502,10 @@ __device__ __forceinline__ void gene_reduce_item(const void* __restrict__ pay, i
     const int j0 = t * kItems;
     const int my_n = cnt - j0 < 0 ? 0 : (cnt - j0 < kItems ? cnt - j0 : kItems);
     {
+      // a run continues into this sub-tile if it starts with the run's gene and its byte
+      // counters have room for kItems more payloads
       const int first = my_n > 0 ? (int)F::item(s_sorted[F::slot(j0)], g0).lg : cur;
-      const bool changed = cur >= 0 && first != cur;
+      const bool changed = cur >= 0 && (first != cur || acc.n > kRunCap - kItems);
       if (__ballot(changed)) {
         gene_wave_flush<k8>(acc, changed ? cur : -2 - (t & (kWave - 1)), s_cbin, s_lbin);
         if (changed) {

@@ -45,9 +45,9 @@ namespace {
 constexpr int64_t kEntHistMax = 1 << 18;  // entities whose first partition level is planned (k_level1_plan)
 
 struct Layout {
-  size_t tile_cnt, scalars, scan_sums, keys_a, keys_b, vals_a, vals_b, counts, offsets, ent_start, partials;
+  size_t tile_cnt, scalars, scan_sums, pay_a, pay_b, half, counts, offsets, ent_start, partials;
   size_t gcounts, gcursor, gtoff, gwork, dflags, gpay, seen, zero_mito, ent_hist, l1_toff, l1_tslot;
-  size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, bigs, wctl, worder, total;
+  size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, bigs, wctl, worder, wx, total;
   int64_t num_tiles, num_chunks, max_ent, max_gene_work, max_seg, max_work;
   int n_buckets;
   bool gene;
@@ -74,10 +74,11 @@ Layout layout_for(const sct_plan_t* plan) {
   L.tile_cnt = take(sizeof(uint64_t) * (size_t)(L.num_tiles + 1));
   L.scalars = take(256);
   L.scan_sums = take(sizeof(uint64_t) * (size_t)(L.num_chunks + 1));
-  L.keys_a = take(sizeof(uint64_t) * (size_t)n1);
-  L.keys_b = take(sizeof(uint64_t) * (size_t)n1);
-  L.vals_a = take(sizeof(uint64_t) * (size_t)n1);  // bucket payload w1 (u64); global sort: u32 values
-  L.vals_b = take(sizeof(uint64_t) * (size_t)n1);
+  // the bucket path's 16-byte payloads (Pay), ping-pong A / B; the global-sort path splits each
+  // into its keys (u64) and values (u32): A = [keys a | values a], B = [keys b | values b]
+  L.half = align_up(sizeof(uint64_t) * (size_t)n1);
+  L.pay_a = take(2 * L.half);
+  L.pay_b = take(2 * L.half);
   L.counts = take(sizeof(uint32_t) * (size_t)m);
   L.offsets = take(sizeof(uint32_t) * (size_t)m);
   L.ent_start = take(sizeof(int64_t) * (size_t)(L.max_ent + 1));
@@ -112,6 +113,7 @@ Layout layout_for(const sct_plan_t* plan) {
   const bool welford = plan->float_mode == SCT_FLOAT_WELFORD;
   L.wctl = take(welford ? sizeof(WelfordCtl) : 0);
   L.worder = take(welford ? sizeof(uint32_t) * (size_t)L.max_ent : 0);
+  L.wx = take(welford ? sizeof(double) * 4 * (size_t)n1 : 0);  // every record's stream values
   L.total = off;
   return L;
 }
@@ -183,16 +185,16 @@ int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool du
 
 template <bool kWideK1>
 int launch_hash_tile(bool cell, bool gene, dim3 grid, hipStream_t s, const uint16_t* bdesc, const uint32_t* bent,
-                     const uint64_t* ka, const uint64_t* va, const uint64_t* kb, const uint64_t* vb, int64_t n,
+                     const Pay* pa, const Pay* pb, int64_t n,
                      const Bits& b, int64_t* partials, uint16_t* dflags) {
   if (cell && gene) {
-    LAUNCH_N("hash_tile", n, (k_hash_tile<true, true, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb, n,
+    LAUNCH_N("hash_tile", n, (k_hash_tile<true, true, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, pa, pb, n,
            b, partials, dflags);
   } else if (cell) {
-    LAUNCH_N("hash_tile", n, (k_hash_tile<true, false, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb, n,
+    LAUNCH_N("hash_tile", n, (k_hash_tile<true, false, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, pa, pb, n,
            b, partials, dflags);
   } else {
-    LAUNCH_N("hash_tile", n, (k_hash_tile<false, false, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, ka, va, kb, vb,
+    LAUNCH_N("hash_tile", n, (k_hash_tile<false, false, kWideK1>), grid, dim3(kHBlock), s, bdesc, bent, pa, pb,
            n, b, partials, dflags);
   }
   return SCT_OK;
@@ -236,10 +238,8 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
                     const uint8_t* mito, const Bits& b, bool cell, bool gene, int64_t* partials, uint16_t* dflags,
                     bool planned, hipStream_t s) {
   if (n == 0) return SCT_OK;
-  uint64_t* ka = at<uint64_t>(ws, L.keys_a);
-  uint64_t* kb = at<uint64_t>(ws, L.keys_b);
-  uint64_t* va = at<uint64_t>(ws, L.vals_a);
-  uint64_t* vb = at<uint64_t>(ws, L.vals_b);
+  Pay* pa = at<Pay>(ws, L.pay_a);
+  Pay* pb = at<Pay>(ws, L.pay_b);
   uint16_t* bdesc = at<uint16_t>(ws, L.bdesc);
   uint32_t* bent = at<uint32_t>(ws, L.bent);
   Seg* seg[2] = {at<Seg>(ws, L.seg_a), at<Seg>(ws, L.seg_b)};
@@ -273,12 +273,10 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     const int bits = KB - depth < kRadixBits ? KB - depth : kRadixBits;
     const int shift = KB - depth - bits + kKeyShift;
     const int src = (level - 1) & 1;
-    const uint64_t* kin = src ? kb : ka;
-    const uint64_t* vin = src ? vb : va;
-    uint64_t* kout = src ? ka : kb;
-    uint64_t* vout = src ? va : vb;
+    const Pay* pin = src ? pb : pa;
+    Pay* pout = src ? pa : pb;
     HIPCHK(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kRadix * (size_t)h.n_seg, s));
-    LAUNCH_N("bucket_hist", h.n_rec, k_bucket_hist, dim3(h.n_work), dim3(kBlock), s, kin, (const Seg*)seg[c],
+    LAUNCH_N("bucket_hist", h.n_rec, k_bucket_hist, dim3(h.n_work), dim3(kBlock), s, pin, (const Seg*)seg[c],
            (const Work*)work[c], shift, bits, hist);
     HIPCHK(hipMemsetAsync(ctl, 0, 3 * sizeof(uint32_t), s));  // next level's n_seg, n_work, n_rec
     LAUNCH("bucket_classify", k_bucket_classify, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c], hist, cur, depth,
@@ -287,7 +285,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     // the next level's counts are final after classify: read them while the scatter runs
     if (int rb = readback_start(ctl, sizeof(h), s)) return rb;
     const uint32_t n_work = h.n_work;
-    LAUNCH_N("bucket_scatter", h.n_rec, k_bucket_scatter, dim3(n_work), dim3(kSBlock), s, kin, vin, kout, vout,
+    LAUNCH_N("bucket_scatter", h.n_rec, k_bucket_scatter, dim3(n_work), dim3(kSBlock), s, pin, pout,
            (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
     if (int rb = readback_finish(&h, sizeof(h))) return rb;
     c ^= 1;
@@ -297,16 +295,16 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   const dim3 tgrid((unsigned)cdiv(n, kWin));
   int rc;
   if (b.k1 > kNarrowK1Bits) {
-    rc = launch_hash_tile<true>(cell, gene, tgrid, s, bdesc, bent, ka, va, kb, vb, n, b, partials, dflags);
+    rc = launch_hash_tile<true>(cell, gene, tgrid, s, bdesc, bent, pa, pb, n, b, partials, dflags);
   } else {
-    rc = launch_hash_tile<false>(cell, gene, tgrid, s, bdesc, bent, ka, va, kb, vb, n, b, partials, dflags);
+    rc = launch_hash_tile<false>(cell, gene, tgrid, s, bdesc, bent, pa, pb, n, b, partials, dflags);
   }
   if (rc) return rc;
   if (h.n_big > 0) {
     const dim3 bgrid(h.n_big);
     const bool wide = b.k1 > kNarrowK1Bits;
 #define SCT_BIG(C, G, W)                                                                                          \
-  LAUNCH_N("big_bucket", h.n_big_rec, (k_big_bucket<C, G, W>), bgrid, dim3(kBigBlock), s, (const Seg*)bigs, ka, va, kb, vb, b, \
+  LAUNCH_N("big_bucket", h.n_big_rec, (k_big_bucket<C, G, W>), bgrid, dim3(kBigBlock), s, (const Seg*)bigs, pa, pb, b, \
          partials, dflags)
     if (cell && gene) {
       if (wide) { SCT_BIG(true, true, true); } else { SCT_BIG(true, true, false); }
@@ -320,14 +318,14 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   if (h.n_giant > 0) {
     const dim3 ggrid(h.n_giant);
     if (cell && gene) {
-      LAUNCH("bucket_giant", (k_bucket_giant<true, true>), ggrid, dim3(kBlock), s, (const Seg*)giants, ka, va, kb,
-             vb, partials, dflags);
+      LAUNCH("bucket_giant", (k_bucket_giant<true, true>), ggrid, dim3(kBlock), s, (const Seg*)giants, pa, pb,
+             partials, dflags);
     } else if (cell) {
-      LAUNCH("bucket_giant", (k_bucket_giant<true, false>), ggrid, dim3(kBlock), s, (const Seg*)giants, ka, va, kb,
-             vb, partials, dflags);
+      LAUNCH("bucket_giant", (k_bucket_giant<true, false>), ggrid, dim3(kBlock), s, (const Seg*)giants, pa, pb,
+             partials, dflags);
     } else {
-      LAUNCH("bucket_giant", (k_bucket_giant<false, false>), ggrid, dim3(kBlock), s, (const Seg*)giants, ka, va, kb,
-             vb, partials, dflags);
+      LAUNCH("bucket_giant", (k_bucket_giant<false, false>), ggrid, dim3(kBlock), s, (const Seg*)giants, pa, pb,
+             partials, dflags);
     }
   }
   return SCT_OK;
@@ -409,8 +407,8 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
              (uint32_t)plan->n_umi_ids};
   RecCols rc2{rec->ref, rec->pos, rec->gq_sum, rec->gq_len, rec->gq_gt30, rec->bits, rec->xf,
               rec->cy_gt30, rec->cy_len, rec->uy_gt30, rec->uy_len};
-  SortBuffers B{at<uint64_t>(ws, L.keys_a), at<uint64_t>(ws, L.keys_b), at<uint32_t>(ws, L.vals_a),
-                at<uint32_t>(ws, L.vals_b), at<uint32_t>(ws, L.counts), at<uint32_t>(ws, L.offsets),
+  SortBuffers B{at<uint64_t>(ws, L.pay_a), at<uint64_t>(ws, L.pay_b), at<uint32_t>(ws, L.pay_a + L.half),
+                at<uint32_t>(ws, L.pay_b + L.half), at<uint32_t>(ws, L.counts), at<uint32_t>(ws, L.offsets),
                 at<uint64_t>(ws, L.scan_sums)};
   int64_t* ent_start = at<int64_t>(ws, L.ent_start);
   int64_t* partials = at<int64_t>(ws, L.partials);
@@ -423,8 +421,8 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
                        !(nol1 && nol1[0] == '1');
   L1Plan l1{};
   if (planned)
-    l1 = L1Plan{at<uint32_t>(ws, L.ent_hist), at<uint32_t>(ws, L.l1_toff), at<uint2>(ws, L.l1_tslot), B.kb,
-                at<uint64_t>(ws, L.vals_b)};
+    l1 = L1Plan{at<uint32_t>(ws, L.ent_hist), at<uint32_t>(ws, L.l1_toff), at<uint2>(ws, L.l1_tslot),
+                at<Pay>(ws, L.pay_b)};
   const uint8_t* mito = gene_is_mito;
   if (cell && !mito) {
     uint8_t* z = at<uint8_t>(ws, L.zero_mito);
@@ -450,10 +448,10 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   uint32_t* gwide = reinterpret_cast<uint32_t*>(at<uint64_t>(ws, L.scalars) + 16);
   HIPCHK(hipMemsetAsync(gwide, streams ? 0 : 1, sizeof(uint32_t), s));
   if (bucket) {
-    uint64_t* va = at<uint64_t>(ws, L.vals_a);
-    rc = streams ? launch_build_keys<true, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
+    uint64_t* pay = at<uint64_t>(ws, L.pay_a);  // (the bucket path writes Pay records through `keys`)
+    rc = streams ? launch_build_keys<true, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, pay, nullptr, ent_start,
                                                  partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff, l1)
-                 : launch_build_keys<true, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, va, ent_start,
+                 : launch_build_keys<true, false>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, pay, nullptr, ent_start,
                                                   partials, gcounts, L.n_buckets, &ctl->err, gwide, gtoff, l1);
   } else {
     rc = streams ? launch_build_keys<false, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, B.ka, B.va,
@@ -508,12 +506,16 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
         LAUNCH("welford_bins", k_welford_bins, egrid, dim3(kBlock), s, (const int64_t*)ent_start, n_ent, n, wc);
         LAUNCH("welford_order", k_welford_order, egrid, dim3(kBlock), s, (const int64_t*)ent_start, n_ent, n, wc,
                worder);
+        double* xs = at<double>(ws, L.wx);
+        const dim3 xgrid((unsigned)cdiv(n, kBlock));
         if (cell) {
-          LAUNCH("welford_wave", k_welford_wave<true>, dim3(kWfBlocks), dim3(kBlock), s, rc2,
-                 (const int64_t*)ent_start, n_ent, n, (const uint32_t*)worder, wc, out_f);
+          LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s, rc2, n, xs);
+          LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s,
+                   (const int64_t*)ent_start, n_ent, n, (const uint32_t*)worder, wc, (const double*)xs, out_f);
         } else {
-          LAUNCH("welford_wave", k_welford_wave<false>, dim3(kWfBlocks), dim3(kBlock), s, rc2,
-                 (const int64_t*)ent_start, n_ent, n, (const uint32_t*)worder, wc, out_f);
+          LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s, rc2, n, xs);
+          LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfBlocks), dim3(kBlock), s,
+                   (const int64_t*)ent_start, n_ent, n, (const uint32_t*)worder, wc, (const double*)xs, out_f);
         }
       }
       if (cell) {

@@ -131,34 +131,31 @@ struct AddAcc {
   }
 };
 
-// s_e16 holds, per tile position, the run index relative to the run before the tile's first
-// head (local 0 = the run continuing from the previous tile), two pad halves after every 32: the
-// blocked passes (thread t reads positions 32t .. 32t+31, 17 words apart) then hit distinct banks.
-__device__ __forceinline__ int epad(int q) { return q + 2 * (q >> 5); }
+
 // The key pass (k_build_keys_run) owns kKTile records per block, kKItems per thread: twice the
 // heads tile (k_heads / tile offsets are per kTile), which halves the per-block costs (run-id
 // scan, the wave flushes that end each quality stream, the gene-bucket histogram flush).
 constexpr int kKItems = 2 * kItems;  // 32: the blocked head masks are 32-bit
 constexpr int kKTile = kBlock * kKItems;
 constexpr int kKTilesPerBlock = kKTile / kTile;
-constexpr int kTilePad = kKTile + 2 * (kKTile / 32);
 constexpr int kRunBatch = 8;  // striped rounds whose entity loads are in flight together
-static_assert(kKItems <= 32, "head masks are 32-bit");
+static_assert(kKItems == 32, "head masks are 32-bit; two threads per 64-position word of s_hb");
 static_assert(kKItems % kRunBatch == 0, "whole batches");
 static_assert(kKTile <= 65535, "local run ids are 16-bit");
 
-// Number the runs of the tile: s_e16[epad(q)] = run index of tile position q minus the returned
-// base (tile_off - 1).  Heads are found on striped, coalesced loads (the previous record comes
-// from the neighbouring lane; lane 0 re-reads it, a cache hit) and kept as one bit per position
-// (s_hb: kKTile / 64 words, ballots); each thread then numbers its 32 blocked positions from its
-// word of the mask and a block scan.  Writes ent_start[run] for heads when ent_start is set.
-// Block-wide (barriers).
+// Number the runs of the tile.  Run ids are local: the run of tile position q is the returned base
+// (tile_off - 1) plus the number of heads at positions <= q (local 0 = the run continuing from the
+// previous tile).  Heads are found on striped, coalesced loads (the previous record comes from the
+// neighbouring lane; lane 0 re-reads it, a cache hit) and kept as one bit per position (s_hb:
+// kKTile / 64 words, ballots); a block scan counts each thread's 32 blocked positions' heads, and
+// s_wpre gets the heads before each 64-position word, so loc_of() reads any position's run id off
+// two LDS words.  Writes ent_start[run] for heads when ent_start is set.  Block-wide (barriers).
 // Also returns the thread's blocked head mask (*my_heads) and the local id of the run before its
 // first position (*my_ex): the run of position 32t + j is ebase + my_ex + popc(heads & bits 0..j).
 __device__ __forceinline__ int64_t tile_run_ids(const int32_t* __restrict__ ent, int64_t base, int tile_n,
-                                                uint64_t tile_off, uint16_t* s_e16, uint64_t* s_hb,
-                                                uint64_t* s_scan, int64_t* __restrict__ ent_start,
-                                                uint32_t* my_heads, uint32_t* my_ex, uint32_t* n_heads) {
+                                                uint64_t tile_off, uint64_t* s_hb, uint64_t* s_scan,
+                                                int64_t* __restrict__ ent_start, uint32_t* my_heads,
+                                                uint32_t* my_ex, uint32_t* n_heads, uint16_t* s_wpre) {
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
   for (int j0 = 0; j0 < kKItems; j0 += kRunBatch) {
     int32_t v[kRunBatch], pv[kRunBatch];
@@ -187,24 +184,24 @@ __device__ __forceinline__ int64_t tile_run_ids(const int32_t* __restrict__ ent,
   *my_heads = heads;
   *my_ex = (uint32_t)ex;
   *n_heads = (uint32_t)tot;  // the tile's last run has local id n_heads
-  uint32_t loc = (uint32_t)ex;
-  const int q0 = t * kKItems;
-  uint32_t* s_w = reinterpret_cast<uint32_t*>(s_e16);
-#pragma unroll
-  for (int j = 0; j < kKItems; j += 2) {  // two positions per 32-bit store (epad(q0 + j) is even)
-    uint32_t l2[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      if ((heads >> (j + k)) & 1u) {
-        loc += 1;
-        if (ent_start) ent_start[ebase + loc] = base + q0 + j + k;
-      }
-      l2[k] = loc;
+  if (!(t & 1)) s_wpre[t >> 1] = (uint16_t)ex;  // thread 2i starts word i (kKItems == 32)
+  if (ent_start) {
+    const int q0 = t * kKItems;
+    for (uint32_t hb = heads; hb; hb &= hb - 1) {
+      const int j = __ffs(hb) - 1;
+      ent_start[ebase + (uint32_t)ex + (uint32_t)__popc(heads & ((2u << j) - 1u))] = base + q0 + j;
     }
-    if (q0 + j < tile_n) s_w[epad(q0 + j) / 2] = l2[0] | (l2[1] << 16);
   }
   __syncthreads();
   return ebase;
+}
+
+// The local run id of tile position q (tile_run_ids' convention) from the head bits: the heads
+// before q's 64-position word plus those of the word at positions <= q.
+__device__ __forceinline__ uint32_t loc_of(int q, const uint64_t* s_hb, const uint16_t* s_wpre) {
+  const uint64_t m = s_hb[q >> 6];
+  const int bit = q & 63;
+  return (uint32_t)s_wpre[q >> 6] + (uint32_t)__popcll(bit == 63 ? m : (m & ((2ull << bit) - 1ull)));
 }
 
 // ---- the first partition level, planned before the key pass (bucket.h) ----
@@ -230,8 +227,7 @@ struct L1Plan {
   uint32_t* hist;  // [entity][kRadix] (nullptr: payloads are written in input order)
   uint32_t* toff;  // [tile][kL1Slots][kRadix]: the tile's offset inside each child it feeds
   uint2* tslot;    // [tile]: the slots' local run ids, 16 bits each (kL1NoSlot: none)
-  uint64_t* keys_b;  // the level-1 children's buffer (B)
-  uint64_t* vals_b;
+  Pay* pay_b;      // the level-1 children's buffer (B)
 };
 __device__ __forceinline__ uint32_t l1_slot_loc(uint2 ts, int k) {
   return ((k < 2 ? ts.x : ts.y) >> (16 * (k & 1))) & 0xffffu;
@@ -249,9 +245,9 @@ __global__ void __launch_bounds__(kBlock) k_level1_plan(const int32_t* __restric
                                                         uint32_t n_k1, int64_t n, const uint64_t* __restrict__ tile_off,
                                                         Bits b, int dshift, int64_t* __restrict__ ent_start,
                                                         L1Plan l1) {
-  __shared__ uint16_t s_e16[kTilePad];
   __shared__ uint64_t s_scan[kWaves + 1];
   __shared__ uint64_t s_hb[kKTile / 64];
+  __shared__ uint16_t s_wpre[kKTile / 64];
   __shared__ uint32_t s_h[kL1Slots * kRadix];
   __shared__ uint32_t s_slot[kL1Slots];
   __shared__ uint32_t s_nmid;
@@ -263,15 +259,15 @@ __global__ void __launch_bounds__(kBlock) k_level1_plan(const int32_t* __restric
   if (t < kL1Slots) s_slot[t] = kL1NoSlot;
   if (t == 0) s_nmid = 0;
   uint32_t heads, ex, n_heads;  // (tile_run_ids' barriers publish the initialisation above)
-  const int64_t ebase = tile_run_ids(ent, base, tile_n, tile_off[(size_t)blockIdx.x * kKTilesPerBlock], s_e16, s_hb,
-                                     s_scan, ent_start, &heads, &ex, &n_heads);
-  const uint32_t first = s_e16[epad(0)];  // the run at the tile's first position
+  const int64_t ebase = tile_run_ids(ent, base, tile_n, tile_off[(size_t)blockIdx.x * kKTilesPerBlock], s_hb,
+                                     s_scan, ent_start, &heads, &ex, &n_heads, s_wpre);
+  const uint32_t first = loc_of(0, s_hb, s_wpre);  // the run at the tile's first position
   // inner runs with more than kBigCap records in the tile: head h and position h + kBigCap in one run
   for (uint32_t hb = heads; hb; hb &= hb - 1) {
     const int j = __ffs(hb) - 1;
     const uint32_t l = ex + (uint32_t)__popc(heads & ((2u << j) - 1u));
     const int h = t * kKItems + j;
-    if (l != first && l != n_heads && h + kBigCap < tile_n && s_e16[epad(h + kBigCap)] == l) {
+    if (l != first && l != n_heads && h + kBigCap < tile_n && loc_of(h + kBigCap, s_hb, s_wpre) == l) {
       const uint32_t k = atomicAdd(&s_nmid, 1u);
       if (k < kL1Slots - 2) s_slot[1 + k] = l;
     }
@@ -296,7 +292,7 @@ __global__ void __launch_bounds__(kBlock) k_level1_plan(const int32_t* __restric
       const int q = (j0 + u) * kBlock + t;
       if (q >= tile_n) continue;
       const uint32_t k1 = v[u] < n_k1 ? v[u] : 0u;  // the key pass's rule for an invalid id
-      const int k = slot_of(s_e16[epad(q)], sl);
+      const int k = slot_of(loc_of(q, s_hb, s_wpre), sl);
       if (k >= 0) atomicAdd(&s_h[k * kRadix + (b.scramble(k1) >> dshift)], 1u);
     }
   }
@@ -467,16 +463,24 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
 
 // kBucket: write the bucket path's 16-byte payload (bucket.h: w0 = key' | ref | strand |
 // mapped, w1 = index | pos; a mapped ref id >= 2^kRefBits raises *err): a segment's record (l1.hist
-// set: the first partition level planned by k_level1_plan) straight into its level-1 child in buffer
-// B, any other record at its own position in buffer A.  Otherwise the global sort's (key with entity
+// set: the first partition level planned by k_level1_plan) into its level-1 child in buffer B, any
+// other record at its own position in buffer A.  Otherwise the global sort's (key with entity
 // bits, u32 value with bit 31 = unmapped).
+// Segment records are staged per batch of kKeyBatch rounds (kStage records): ranked in LDS by
+// (batch slot, digit), placed in child order, and written out as contiguous runs per child -- a
+// wave's store then covers a few runs instead of 64 scattered lines.  A batch holds at most two
+// segment runs (its first and its last: a run inside it has < kStage <= kBigCap records).
 // kStreams: also the exact quality-stream lanes of the runs (stream_tile), reusing the tile's
 // run ids: the stream ALU work overlaps the key pass's memory traffic in one launch.
 constexpr int kKeyBatch = 4;  // striped rounds whose column loads are issued together (8: occupancy 3, slower)
+constexpr int kStage = kKeyBatch * kBlock;
 static_assert(kKItems % kKeyBatch == 0, "whole batches");
+static_assert(kStage <= kBigCap, "a run inside a batch is never a segment");
+static_assert(kStage < (1 << 16), "16-bit ranks");
+constexpr uint32_t kDirect = 0xffffffffu;
 
 template <bool kCell, bool kGene, bool kBucket, bool kStreams>
-// 5 waves per SIMD (<= 96 VGPRs; 3 dwords spill, off the per-record loops)
+// 5 waves per SIMD (<= 96 VGPRs)
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) k_build_keys_run(KeyCols c, RecCols r, const uint8_t* __restrict__ k1_is_mito,
                                                            int64_t n, const uint64_t* __restrict__ tile_off, Bits b,
                                                            uint64_t* __restrict__ keys, void* __restrict__ vals,
@@ -486,9 +490,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
                                                            uint32_t* __restrict__ err, uint32_t* __restrict__ gwide,
                                                            uint32_t* __restrict__ gtoff, L1Plan l1) {
   static_assert(!kGene || kCell, "gene buckets come from the cell view");
-  __shared__ uint16_t s_e16[kTilePad];
   __shared__ uint64_t s_scan[kWaves + 1];
-  __shared__ uint64_t s_hb[kKTile / 64];  // tile_run_ids' head bits
+  __shared__ uint64_t s_hb[kKTile / 64];      // tile_run_ids' head bits
+  __shared__ uint16_t s_wpre[kKTile / 64];    // heads before each word of s_hb (loc_of)
   using TabT = typename std::conditional<kStreams, StreamTabs, uint32_t>::type;
   __shared__ TabT s_tab_[1];
   StreamTabs* s_tab = reinterpret_cast<StreamTabs*>(s_tab_);
@@ -504,15 +508,23 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
     fill_stream_tabs<kCell>(r, base, s_tab);
   }
   // level-1 children (l1.hist set): per slot whose run is a segment, the next position of each
-  // child inside this tile's range; s_lslot = the slot's local run id, or kL1NoSlot
-  __shared__ uint32_t s_pos[kBucket ? kL1Slots * kRadix : 1];
+  // child inside this tile's range; s_lslot = the slot's local run id, or kL1NoSlot.  A batch's
+  // staging: s_bc counts, then child-order starts, per (batch slot, digit); s_gd the distance from
+  // a staged position to its destination.
+  constexpr int kL1 = kBucket ? 1 : 0;
+  __shared__ uint32_t s_pos[kL1 ? kL1Slots * kRadix : 1];
   __shared__ uint32_t s_lslot[kL1Slots];
+  __shared__ Pay s_stage[kL1 ? kStage : 1];
+  __shared__ uint32_t s_bc[kL1 ? 2 * kRadix : 1];
+  __shared__ uint32_t s_gd[kL1 ? 2 * kRadix : 1];
   const int KB = b.k1 + b.k2 + b.h;
   const int bits1 = KB < kRadixBits ? KB : kRadixBits;
   const int sh1 = KB - bits1;
+  const uint32_t dmask = (1u << bits1) - 1u;
   const uint64_t tile_off0 = tile_off[(size_t)blockIdx.x * kKTilesPerBlock];
+  const bool planned = kBucket && l1.hist != nullptr;  // uniform
   if constexpr (kBucket) {
-    if (l1.hist) {
+    if (planned) {
       static_assert(kBlock == kRadix, "one thread per digit");
       const uint2 ts = l1.tslot[blockIdx.x];
 #pragma unroll
@@ -526,15 +538,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
         }
         if (t == 0) s_lslot[k] = seg ? l : kL1NoSlot;
       }
+      s_bc[t] = 0;
+      s_bc[kRadix + t] = 0;
     }
   }
   // 1-2. run index of every record of the tile
   uint32_t my_heads, my_ex, n_heads;
-  const int64_t ebase = tile_run_ids(c.ent, base, tile_n, tile_off0, s_e16, s_hb, s_scan,
-                                     (kBucket && l1.hist) ? nullptr : ent_start, &my_heads, &my_ex, &n_heads);
+  const int64_t ebase = tile_run_ids(c.ent, base, tile_n, tile_off0, s_hb, s_scan, planned ? nullptr : ent_start,
+                                     &my_heads, &my_ex, &n_heads, s_wpre);
   uint32_t lsl[kL1Slots];
 #pragma unroll
-  for (int k = 0; k < kL1Slots; k++) lsl[k] = (kBucket && l1.hist) ? s_lslot[k] : kL1NoSlot;
+  for (int k = 0; k < kL1Slots; k++) lsl[k] = planned ? s_lslot[k] : kL1NoSlot;
 
   // 3. striped pass: keys, values and the run's additive metrics.  Runs are contiguous, so
   // in a round the wave's lanes cross a run boundary together: flush wave-cooperatively.
@@ -546,6 +560,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
   // The columns of kKeyBatch rounds are loaded together (clamped, unconditional loads: all in
   // flight at once), then the rounds are processed: the wait for memory is paid once per batch.
   for (int j0 = 0; j0 < kKItems; j0 += kKeyBatch) {
+    const int qlo = j0 * kBlock;
+    if (qlo >= tile_n) break;  // block-uniform
     int32_t vk1[kKeyBatch], vk2[kKeyBatch], vref[kKeyBatch], vpos[kKeyBatch];
     uint8_t vbt[kKeyBatch], vxf[kKeyBatch];
 #pragma unroll
@@ -569,10 +585,60 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
       const int wo = t & ~(kWave - 1) & (kBlock - 1);
       const int lo = (j0 == 0 ? 0 : (j0 - 1) * kBlock) + wo;
       const int hi = (j0 + kKeyBatch - 1) * kBlock + wo + kWave - 1;
-      const int elo = __builtin_amdgcn_readfirstlane((int)s_e16[epad(lo)]);
-      const int ehi = __builtin_amdgcn_readfirstlane((int)s_e16[epad(hi)]);
+      const int elo = __builtin_amdgcn_readfirstlane((int)loc_of(lo, s_hb, s_wpre));
+      const int ehi = __builtin_amdgcn_readfirstlane((int)loc_of(hi, s_hb, s_wpre));
       one_run = elo == ehi;
       if (one_run) cur_e = ebase + elo;
+    }
+    // the batch's segment runs (block-uniform): its first and its last run, if segments
+    uint32_t blo = kL1NoSlot, bhi = kL1NoSlot;
+    int bs0 = -1, bs1 = -1;
+    if (planned) {
+      const int qhi = (qlo + kStage < tile_n ? qlo + kStage : tile_n) - 1;
+      blo = loc_of(qlo, s_hb, s_wpre);
+      bhi = loc_of(qhi, s_hb, s_wpre);
+      bs0 = slot_of(blo, lsl);
+      bs1 = bhi != blo ? slot_of(bhi, lsl) : -1;
+    }
+    const bool stage = bs0 >= 0 || bs1 >= 0;
+    uint32_t rk[kKeyBatch];  // staged records: batch slot << 16 | rank in (slot, digit); else kDirect
+    uint32_t t0 = 0, n_staged = 0;
+    if constexpr (kBucket) {
+      if (stage) {
+#pragma unroll
+        for (int u = 0; u < kKeyBatch; u++) {
+          const int q = (j0 + u) * kBlock + t;
+          rk[u] = kDirect;
+          if (q >= tile_n) continue;
+          const uint32_t loc = one_run ? (uint32_t)(cur_e - ebase) : loc_of(q, s_hb, s_wpre);
+          const int ls = (loc == blo && bs0 >= 0) ? 0 : (loc == bhi && bs1 >= 0) ? 1 : -1;
+          if (ls < 0) continue;
+          const uint32_t k1 = (uint32_t)vk1[u] < c.n_k1 ? (uint32_t)vk1[u] : 0u;  // (the rule below)
+          const uint32_t dg = (uint32_t)(((uint64_t)b.scramble(k1) << (b.k2 + b.h)) >> sh1) & dmask;
+          rk[u] = ((uint32_t)ls << 16) | atomicAdd(&s_bc[ls * kRadix + dg], 1u);
+        }
+        __syncthreads();
+        // child-order starts per (batch slot, digit); the tile's child positions advance
+        const uint32_t c0 = s_bc[t], c1 = s_bc[kRadix + t];
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan<uint64_t>((uint64_t)c0 | ((uint64_t)c1 << 32), &tot, s_scan);
+        t0 = (uint32_t)tot;
+        n_staged = t0 + (uint32_t)(tot >> 32);
+        const uint32_t st0 = (uint32_t)ex, st1 = t0 + (uint32_t)(ex >> 32);
+        s_bc[t] = st0;
+        s_bc[kRadix + t] = st1;
+        if (c0) {  // thread t alone owns digit t of the batch's slots
+          const uint32_t g = s_pos[bs0 * kRadix + t];
+          s_pos[bs0 * kRadix + t] = g + c0;
+          s_gd[t] = g - st0;
+        }
+        if (c1) {
+          const uint32_t g = s_pos[bs1 * kRadix + t];
+          s_pos[bs1 * kRadix + t] = g + c1;
+          s_gd[kRadix + t] = g - st1;
+        }
+        __syncthreads();
+      }
     }
 #pragma unroll
     for (int u = 0; u < kKeyBatch; u++) {
@@ -581,7 +647,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
       const int64_t p = base + q;
       int64_t e = cur_e;
       if (!one_run) {
-        e = valid ? ebase + (int64_t)s_e16[epad(q)] : cur_e;
+        e = valid ? ebase + (int64_t)loc_of(q, s_hb, s_wpre) : cur_e;
         wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
         if (!valid) continue;
         cur_e = e;
@@ -603,23 +669,20 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
       if constexpr (kBucket) {
         const bool mito = kCell ? k1_is_mito[k1] != 0 : false;
         const uint64_t kp = make_key(0, k1, k2, hsh, b);
-        const uint64_t w0 = payload_w0(kp, ref, rev, mapped, mito);
-        const uint64_t w1 = ((uint64_t)p << 32) | (uint32_t)pos;
-        const int sl = slot_of((uint32_t)(e - ebase), lsl);
-        if (sl >= 0) {
-          const uint32_t dg = (uint32_t)(kp >> sh1) & ((1u << bits1) - 1u);
-          const uint32_t dst = atomicAdd(&s_pos[sl * kRadix + dg], 1u);
-          l1.keys_b[dst] = w0;
-          l1.vals_b[dst] = w1;
+        const Pay x{payload_w0(kp, ref, rev, mapped, mito), ((uint64_t)p << 32) | (uint32_t)pos};
+        if (stage && rk[u] != kDirect) {
+          const uint32_t ls = rk[u] >> 16;
+          const uint32_t dg = (uint32_t)(kp >> sh1) & dmask;
+          s_stage[s_bc[ls * kRadix + dg] + (rk[u] & 0xffffu)] = x;
         } else {
-          keys[p] = w0;
-          static_cast<uint64_t*>(vals)[p] = w1;
+          reinterpret_cast<Pay*>(keys)[p] = x;  // (the bucket path's keys are payload buffer A)
         }
         if (mapped && (uint32_t)ref >= (1u << kRefBits)) atomicOr(err, 1u);
       } else {
         keys[p] = make_key((uint64_t)e, k1, k2, hsh, b);
         static_cast<uint32_t*>(vals)[p] = (uint32_t)p | (mapped ? 0u : kUnmappedValBit);
       }
+      if (kGene) atomicAdd(&s_hist[k1 / kGenesPerBucket], 1u);
       // MetricAggregator.parse_molecule (aggregator.py:259-334)
       acc.v[0] += 1;
       acc.v[1] += (bt & SCT_B_PERFECT_UMI) ? 1 : 0;
@@ -640,7 +703,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
         acc.v[11] += (xf == SCT_XF_ABSENT);
         acc.v[12] += k1_is_mito[k1];
       }
-      if (kGene) atomicAdd(&s_hist[k1 / kGenesPerBucket], 1u);
+    }
+    if constexpr (kBucket) {
+      if (stage) {  // the staged records, child by child (contiguous runs), to buffer B
+        __syncthreads();
+        s_bc[t] = 0;  // (the next batch's counters: every read of the starts is done)
+        s_bc[kRadix + t] = 0;
+        for (uint32_t q = t; q < n_staged; q += kBlock) {
+          const Pay x = s_stage[q];
+          const uint32_t dg = (uint32_t)(x.w0 >> (sh1 + kKeyShift)) & dmask;
+          l1.pay_b[s_gd[(q >= t0 ? kRadix : 0) + dg] + q] = x;
+        }
+        __syncthreads();
+      }
     }
   }
   wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);

@@ -276,7 +276,12 @@ class Engine:
         ms = (ctypes.c_double * cap)()
         launches = (ctypes.c_int64 * cap)()
         items = (ctypes.c_int64 * cap)()
-        k = self.lib.sct_profile_read_items(names, ms, launches, items, cap)
+        if hasattr(self.lib, "sct_profile_read_items"):
+            k = self.lib.sct_profile_read_items(names, ms, launches, items, cap)
+        else:  # an older engine (SCT_LIB_PATH, A/B runs): no item counts
+            k = self.lib.sct_profile_read(names, ms, launches, cap)
+            for i in range(cap):
+                items[i] = -1
         return {names[i].decode(): (float(ms[i]), int(launches[i]), int(items[i])) for i in range(min(k, cap))}
 
 

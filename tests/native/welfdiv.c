@@ -1,8 +1,10 @@
-/* The Welford chain's division in k_welford_wave (sctools_amd/csrc/finalize.h): with
- * y = RN(1/k), q0 = RN(delta * y), r = fma(-q0, k, delta) (exact) and q = RN(q0 + r * y),
- * q must equal the IEEE quotient RN(delta / k) that Python's `mean += delta / count`
- * computes (stats.py:82-87).  Random deltas over 71 binades and both signs, k up to 2^31
- * (uniform, small, near powers of two).  Prints the number of mismatches.
+/* The Welford chain's division (sctools_amd/csrc/finalize.h) must equal the IEEE quotient
+ * RN(delta / k) that Python's `mean += delta / count` computes (stats.py:82-87).  Two forms:
+ *   Markstein:     y = RN(1/k), q0 = RN(delta * y), r = fma(-q0, k, delta) (exact), q = RN(q0 + r * y);
+ *   double-double: y_hi = RN(1/k), y_lo = RN(fma(-k, y_hi, 1) * y_hi), q = fma(delta, y_hi, RN(delta * y_lo))
+ *                  (two dependent operations after delta instead of three).
+ * Random non-zero deltas over 71 binades and both signs, k up to 2^31 (uniform, small, near
+ * powers of two).  Prints the number of mismatches of each form ("markstein double_double").
  * Usage: welfdiv N [seed] */
 #include <math.h>
 #include <stdint.h>
@@ -21,7 +23,7 @@ static uint64_t rnd(void) {
 int main(int argc, char** argv) {
   long n = argc > 1 ? atol(argv[1]) : 1000000;
   if (argc > 2) s ^= (uint64_t)atoll(argv[2]) * 0x9E3779B97F4A7C15ull;
-  long bad = 0;
+  long bad = 0, bad_dd = 0;
   for (long it = 0; it < n; it++) {
     uint64_t u = rnd();
     double k;
@@ -41,11 +43,18 @@ int main(int argc, char** argv) {
     double q0 = delta * y;
     double r = fma(-q0, k, delta);
     double q = fma(r, y, q0);
-    if (q != delta / k) {
+    const double want = delta / k;
+    if (q != want) {
       if (bad < 5) printf("mismatch delta=%a k=%.0f\n", delta, k);
       bad++;
     }
+    const double y_lo = fma(-k, y, 1.0) * y;
+    const double qd = fma(delta, y, delta * y_lo);
+    if (memcmp(&qd, &want, 8) != 0) {
+      if (bad_dd < 5) printf("double-double mismatch delta=%a k=%.0f\n", delta, k);
+      bad_dd++;
+    }
   }
-  printf("%ld\n", bad);
+  printf("%ld %ld\n", bad, bad_dd);
   return 0;
 }

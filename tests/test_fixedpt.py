@@ -110,10 +110,11 @@ def test_division_free_quotient_is_exact():
 
 
 def test_welford_chain_division_is_ieee(tmp_path):
-    """k_welford_wave divides by the record count as RN(q0 + r y) (finalize.h); it must be the
-    IEEE quotient for every delta / k the chain can meet (checked on 20M random cases here)."""
+    """The Welford chains divide by the record count without a division instruction (finalize.h):
+    both the Markstein form RN(q0 + r y) and the double-double form fma(delta, y_hi, RN(delta y_lo))
+    must be the IEEE quotient for every delta / k the chain can meet (20M random cases here)."""
     exe = str(tmp_path / "welfdiv")
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", exe, os.path.join(HERE, "native", "welfdiv.c"), "-lm"],
                    check=True)
     out = subprocess.run([exe, "20000000", "7"], check=True, capture_output=True, text=True).stdout
-    assert out.strip().splitlines()[-1] == "0", out
+    assert out.strip().splitlines()[-1] == "0 0", out
