@@ -7,14 +7,18 @@ HDRS := $(wildcard sctools_amd/csrc/*.h) include/sctools_gpu.h
 
 BAMDEC := sctools_amd/libsct_bam.so
 CSVFMT := sctools_amd/libsct_csv.so
+GBAM := sctools_amd/libsct_gbam.so
 
-all: $(ENGINE) $(BAMDEC) $(CSVFMT) oracle/liboracle.so tests/native/libfxcheck.so
+all: $(ENGINE) $(BAMDEC) $(CSVFMT) $(GBAM) oracle/liboracle.so tests/native/libfxcheck.so
 
 $(ENGINE): $(SRC) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC) -L/opt/rocm/lib -lrccl
 
 $(BAMDEC): sctools_amd/csrc/bamdec.cpp sctools_amd/csrc/bamsplit.cpp sctools_amd/csrc/bgzf.h include/sct_bam.h
 	g++ -O3 -std=c++17 -fopenmp -fPIC -shared -Wall -o $@ sctools_amd/csrc/bamdec.cpp sctools_amd/csrc/bamsplit.cpp -lz
+
+$(GBAM): sctools_amd/csrc/gbam.hip sctools_amd/csrc/inflate.h sctools_amd/csrc/bgzf.h include/sct_gbam.h include/sct_bam.h
+	$(HIPCC) $(HIPFLAGS) -o $@ sctools_amd/csrc/gbam.hip -lz
 
 $(CSVFMT): sctools_amd/csrc/csvfmt.cpp include/sct_csv.h
 	g++ -O3 -std=c++17 -fopenmp -fPIC -shared -Wall -o $@ sctools_amd/csrc/csvfmt.cpp -lz
@@ -26,6 +30,6 @@ tests/native/libfxcheck.so: tests/native/fxcheck.cpp sctools_amd/csrc/fixedpt.h
 	g++ -O2 -std=c++17 -ffp-contract=off -fPIC -shared -o $@ tests/native/fxcheck.cpp
 
 clean:
-	rm -f $(ENGINE) $(BAMDEC) $(CSVFMT) oracle/liboracle.so tests/native/libfxcheck.so
+	rm -f $(ENGINE) $(BAMDEC) $(CSVFMT) $(GBAM) oracle/liboracle.so tests/native/libfxcheck.so
 
 .PHONY: all clean

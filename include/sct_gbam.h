@@ -1,0 +1,70 @@
+/* sct_gbam.h -- BAM -> columnar decode on the device (libsct_gbam.so, HIP for gfx950).
+ *
+ * The same 32-byte SoA columns and dictionaries as include/sct_bam.h's SCT_BAM_CELL_METRICS /
+ * SCT_BAM_GENE_METRICS decode, produced on the GPU: the compressed file is copied to HBM once,
+ * every BGZF member is inflated by one wavefront (Huffman tables and the 32 KB window in LDS),
+ * record starts are found per member and verified against the previous member's walk, each
+ * record is parsed by one lane (the validation of sct_bam.h, the aligned-quality sums, the tag
+ * walk) and the CB / UB / GE strings are interned in device hash tables; only the distinct
+ * strings come back to the host, to be ranked in Python's sorted() order.
+ *
+ * It replaces the same reference reads as sct_bam.h (the per-record pysam loop of
+ * MetricAggregator.parse_molecule, aggregator.py:251-334, and CellMetrics.parse_extra_fields,
+ * aggregator.py:507-530; the native analogue is fastqpreprocessing/src/htslib_tagsort.cpp:106-218).
+ *
+ * The device path handles the common file; anything else -- a record that fails validation, a
+ * typed (non-string) dictionary tag, non-ASCII dictionary bytes, a malformed deflate stream --
+ * makes the call return SCT_GBAM_HOST without raising, and the caller decodes the file with
+ * sct_bam_decode, which reports the reference's exception for the first offending record.
+ */
+#ifndef SCT_GBAM_H
+#define SCT_GBAM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCT_GBAM_HOST 1 /* not decodable on the device as the reference would read it: use sct_bam_decode */
+
+typedef struct sct_gbam sct_gbam_t;
+
+/* Phase 1: map `path`, copy it to device `device`, inflate every BGZF member and locate the
+ * alignment records, on `stream` (a hipStream_t, NULL: the default stream).  On SCT_BAM_OK
+ * *out owns the device buffers and *n_records is the record count.  Returns SCT_GBAM_HOST or an
+ * SCT_BAM_E* code (sct_bam.h) otherwise, with *out NULL. */
+int sct_gbam_open(const char* path, int32_t device, void* stream, sct_gbam_t** out, int64_t* n_records);
+
+/* Phase 2: parse the records into the caller's device columns, in the order of
+ * sct_records_t (include/sctools_gpu.h): cell, umi, gene, ref, pos (int32), gq_sum, gq_len,
+ * gq_gt30 (uint16), bits, xf, cy_gt30, cy_len, uy_gt30, uy_len (uint8); each holds
+ * n_records elements.  metric_mode: SCT_BAM_CELL_METRICS or SCT_BAM_GENE_METRICS.
+ * Returns SCT_BAM_OK, SCT_GBAM_HOST, or SCT_BAM_EIO on a device error. */
+int sct_gbam_parse(sct_gbam_t* h, int32_t metric_mode, void* const* columns);
+
+/* The ranked dictionary `which` (SCT_BAM_TAG_CB / _UB / _GE) after sct_gbam_parse, as
+ * sct_bam_dictionary: *n names, names[i] = bytes[offsets[i] .. offsets[i+1]), entry 0 the
+ * missing tag when *has_none.  Valid until sct_gbam_close. */
+int sct_gbam_dictionary(const sct_gbam_t* h, int32_t which, int64_t* n, const char** bytes,
+                        const int64_t** offsets, int32_t* has_none);
+
+/* Copy `n` inflated bytes from offset `off` of the concatenated BGZF payload to host `dst`
+ * (tests compare it with zlib).  *total (if set) receives the payload length. */
+int sct_gbam_read_inflated(const sct_gbam_t* h, uint64_t off, uint64_t n, void* dst, uint64_t* total);
+
+/* Seconds spent per stage: [0] map + scan, [1] copy to the device, [2] inflate, [3] record
+ * starts, [4] parse + intern, [5] dictionaries, [6] members, [7] record-start repair rounds. */
+int sct_gbam_timing(const sct_gbam_t* h, double* t8);
+
+/* Free the device buffers. */
+void sct_gbam_close(sct_gbam_t* h);
+
+/* Message of the calling thread's last error ("" if none). */
+const char* sct_gbam_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,889 @@
+// gbam.hip -- BAM -> columnar decode on the device (include/sct_gbam.h): libsct_gbam.so.
+//
+//   1. host: map the file, hop the BGZF member headers (bgzf.h scan_blocks), inflate the first
+//      member(s) with zlib only far enough to find where the header ends (H);
+//   2. copy the compressed file to HBM once; k_inflate (inflate.h): one wave per member, every
+//      payload lands at its prefix-sum offset in one contiguous buffer U;
+//   3. record starts: k_guess picks, per member, the first offset from which four records chain
+//      plausibly; k_walk follows block_size from each member's start to the first start in the
+//      next member; a guess that disagrees with the previous member's landing is replaced by it
+//      and the walk repeats (the member holding H starts exactly, so agreement everywhere proves
+//      every start by induction); a second walk writes the record offsets;
+//   4. k_parse: one lane per record -- the validation and fields of bamdec.cpp parse_record
+//      (sct_bam.h), and CB / UB / GE interned in open-addressing tables (one 64-bit CAS per
+//      insert: the string's offset in U, its length and 16 hash bits);
+//   5. per dictionary the occupied slots are compacted, the distinct strings packed and copied to
+//      the host, sorted there (Python's sorted() order, the missing tag first) and the rank of
+//      every slot copied back; k_remap turns slot ids into ranks.
+// Anything the device path does not reproduce exactly returns SCT_GBAM_HOST (the caller decodes
+// with sct_bam_decode, whose first-offending-record error is the reference's exception).
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <hipcub/hipcub.hpp>
+#include <memory>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <vector>
+
+#include "../../include/sct_bam.h"
+#include "../../include/sct_gbam.h"
+#include "bgzf.h"
+#include "inflate.h"
+
+namespace gb {
+
+constexpr uint64_t kUnknown = ~0ull, kBadWalk = ~0ull - 1;
+constexpr uint32_t kScan = 1u << 18;  // bytes a member's start guess looks through
+constexpr uint64_t kPad = 1u << 16;   // readable bytes after the file image and after U
+
+__device__ __forceinline__ uint32_t u16(const uint8_t* U, uint64_t p) { return U[p] | (uint32_t)U[p + 1] << 8; }
+__device__ __forceinline__ uint32_t u32(const uint8_t* U, uint64_t p) {
+  return U[p] | (uint32_t)U[p + 1] << 8 | (uint32_t)U[p + 2] << 16 | (uint32_t)U[p + 3] << 24;
+}
+
+// four records chain from p the way alignment records do (SAM/BAM spec 4.2): a hint only --
+// k_walk's agreement check decides
+__device__ bool plausible(const uint8_t* U, uint64_t ulen, uint64_t p) {
+  for (int j = 0; j < 4; j++) {
+    if (p == ulen) return true;
+    if (p + 36 > ulen) return false;
+    const uint32_t bs = u32(U, p);
+    if (bs < 33 || p + 4 + bs > ulen) return false;
+    const uint64_t d = p + 4;
+    if ((int32_t)u32(U, d) < -1 || (int32_t)u32(U, d + 4) < -1) return false;
+    const uint32_t lrn = U[d + 8];
+    if (lrn == 0 || 32 + lrn > bs || U[d + 32 + lrn - 1] != 0) return false;
+    for (uint32_t q = 0; q + 1 < lrn; q++) {
+      const uint32_t c = U[d + 32 + q];
+      if (c < 33 || c > 126) return false;
+    }
+    const uint64_t need = 32ull + lrn + 4ull * u16(U, d + 12) + (u32(U, d + 16) + 1ull) / 2 + u32(U, d + 16);
+    if (need > bs) return false;
+    p = d + bs;
+  }
+  return true;
+}
+
+// S[m] for members mH < m < n_mem: the first plausible record start at or after O[m]
+__global__ void k_guess(const uint8_t* __restrict__ U, uint64_t ulen, const uint64_t* __restrict__ O, uint32_t mH,
+                        uint32_t n_mem, uint64_t H, uint64_t* __restrict__ S) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m == 0) S[n_mem] = ulen;
+  if (m < mH || m >= n_mem) return;
+  if (m == mH) {
+    S[m] = H;
+    return;
+  }
+  const uint64_t p0 = O[m];
+  uint64_t s = p0 >= ulen ? ulen : kUnknown;
+  const uint64_t e = min(ulen, p0 + kScan);
+  for (uint64_t p = p0; p < e; p++)
+    if (plausible(U, ulen, p)) {
+      s = p;
+      break;
+    }
+  S[m] = s;
+}
+
+// Walk member m's records from S[m] up to the first start at or after O[m+1]: cnt[m] records,
+// land[m+1] the landing (kBadWalk: a record runs past U).  With `starts`, write the offsets.
+__global__ void k_walk(const uint8_t* __restrict__ U, uint64_t ulen, const uint64_t* __restrict__ O, uint32_t mH,
+                       uint32_t n_mem, const uint64_t* __restrict__ S, uint32_t* __restrict__ cnt,
+                       uint64_t* __restrict__ land, uint64_t* __restrict__ starts, const uint64_t* __restrict__ base) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n_mem) return;
+  if (m < mH) {
+    cnt[m] = 0;
+    land[m + 1] = kUnknown;
+    return;
+  }
+  uint64_t p = S[m];
+  if (p == kUnknown) {
+    cnt[m] = 0;
+    land[m + 1] = kUnknown;
+    return;
+  }
+  const uint64_t end = O[m + 1];
+  uint32_t n = 0;
+  uint64_t* out = starts ? starts + base[m] : nullptr;
+  while (p < end) {
+    if (p + 4 > ulen) {
+      p = kBadWalk;
+      break;
+    }
+    const uint64_t bs = u32(U, p);
+    if (p + 4 + bs > ulen) {
+      p = kBadWalk;
+      break;
+    }
+    if (out) out[n] = p;
+    n++;
+    p += 4 + bs;
+  }
+  cnt[m] = n;
+  land[m + 1] = p;
+}
+
+// Replace every start that disagrees with its predecessor's landing; count the disagreements
+// (S[n_mem] = ulen is fixed: a landing elsewhere stays a disagreement).
+__global__ void k_fix(uint32_t mH, uint32_t n_mem, uint64_t* __restrict__ S, const uint64_t* __restrict__ land,
+                      uint32_t* __restrict__ n_bad) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m <= mH || m > n_mem) return;
+  const uint64_t l = land[m];
+  if (l == S[m]) return;
+  if (m < n_mem && l != kUnknown && l != kBadWalk) S[m] = l;
+  atomicAdd(n_bad, 1u);
+}
+
+__global__ void k_u32_to_u64(const uint32_t* __restrict__ a, uint64_t* __restrict__ b, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = a[i];
+}
+
+__global__ void k_any(const uint32_t* __restrict__ st, uint32_t n, uint32_t* __restrict__ flag) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && st[i] != ST_OK) atomicOr(flag, 1u << (st[i] & 15));
+}
+
+// ---------------- record parse ----------------
+// bits / xf codes: include/sctools_gpu.h, sctools_amd/columnar.py
+enum : uint32_t {
+  B_UNMAPPED = 1u << 0, B_REVERSE = 1u << 1, B_DUPLICATE = 1u << 2, B_SPLICED = 1u << 3, B_NH1 = 1u << 4,
+  B_PERFECT_UMI = 1u << 5, B_HAS_CB = 1u << 6, B_PERFECT_CB = 1u << 7
+};
+enum : uint32_t { XF_ABSENT = 0, XF_CODING, XF_INTRONIC, XF_UTR, XF_INTERGENIC, XF_OTHER };
+enum : uint32_t { TV_NONE = 0, TV_STR = 1, TV_INT = 2, TV_RAW = 3 };
+
+struct Cols {
+  int32_t *cell, *umi, *gene, *ref, *pos;
+  uint16_t *gq_sum, *gq_len, *gq_gt30;
+  uint8_t *bits, *xf, *cy_gt30, *cy_len, *uy_gt30, *uy_len;
+};
+
+struct Dicts {
+  unsigned long long* table[3];
+  uint64_t mask[3];
+};
+
+struct DTag {
+  uint32_t kind;  // TV_*
+  uint64_t off;   // value bytes in U (strings)
+  uint32_t n;     // string length
+  int64_t i;      // integer value
+};
+
+__device__ __forceinline__ bool str_eq(const uint8_t* U, uint64_t a, uint64_t b, uint32_t n) {
+  for (uint32_t k = 0; k < n; k++)
+    if (U[a + k] != U[b + k]) return false;
+  return true;
+}
+// Python == of two present tag values where at least one is a string
+__device__ __forceinline__ bool val_eq_str(const uint8_t* U, const DTag& a, const DTag& b) {
+  return a.kind == TV_STR && b.kind == TV_STR && a.n == b.n && str_eq(U, a.off, b.off, a.n);
+}
+__device__ __forceinline__ bool lit_eq(const uint8_t* U, const DTag& v, const char* s, uint32_t n) {
+  if (v.n != n) return false;
+  for (uint32_t k = 0; k < n; k++)
+    if (U[v.off + k] != (uint8_t)s[k]) return false;
+  return true;
+}
+
+// bytes of a tag value of type t at U[p..end) (bgzf.h read_tag), 0 = unknown type or truncated
+__device__ uint32_t tag_value(const uint8_t* U, uint64_t p, uint64_t end, uint32_t t, DTag* v) {
+  const uint64_t room = end > p ? end - p : 0;
+  uint32_t w = 0;
+  switch (t) {
+    case 'Z':
+    case 'H': {
+      uint64_t q = p;
+      while (q < end && U[q]) q++;
+      if (q >= end) return 0;
+      if (v) v->kind = TV_STR, v->off = p, v->n = (uint32_t)(q - p);
+      return (uint32_t)(q - p + 1);
+    }
+    case 'A':
+      if (room < 1) return 0;
+      if (v) v->kind = TV_STR, v->off = p, v->n = 1;
+      return 1;
+    case 'c': case 'C': w = 1; break;
+    case 's': case 'S': w = 2; break;
+    case 'i': case 'I': case 'f': w = 4; break;
+    case 'd': w = 8; break;
+    case 'B': {
+      if (room < 5) return 0;
+      const uint32_t sub = U[p];
+      const uint32_t ew = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2
+                        : (sub == 'i' || sub == 'I' || sub == 'f') ? 4 : 0;
+      if (!ew) return 0;
+      const uint64_t len = 5 + (uint64_t)u32(U, p + 1) * ew;
+      if (len > room) return 0;
+      if (v) v->kind = TV_RAW, v->off = p, v->n = 0;
+      return (uint32_t)len;
+    }
+    default:
+      return 0;
+  }
+  if (w > room) return 0;
+  if (v) {
+    v->off = p, v->n = 0;
+    switch (t) {
+      case 'c': v->kind = TV_INT, v->i = (int8_t)U[p]; break;
+      case 'C': v->kind = TV_INT, v->i = U[p]; break;
+      case 's': v->kind = TV_INT, v->i = (int16_t)u16(U, p); break;
+      case 'S': v->kind = TV_INT, v->i = u16(U, p); break;
+      case 'i': v->kind = TV_INT, v->i = (int32_t)u32(U, p); break;
+      case 'I': v->kind = TV_INT, v->i = u32(U, p); break;
+      default: v->kind = TV_RAW; break;
+    }
+  }
+  return w;
+}
+
+__device__ __forceinline__ uint64_t hash_str(const uint8_t* U, uint64_t off, uint32_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (uint32_t k = 0; k < n; k++) h = (h ^ U[off + k]) * 1099511628211ull;
+  h ^= h >> 29;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 32;
+  return h;
+}
+
+// slot id of the string U[off, off+n) (inserted if new); -1: not internable here (host)
+__device__ int32_t intern(unsigned long long* __restrict__ table, uint64_t mask, const uint8_t* U, uint64_t off,
+                          uint32_t n) {
+  if (n > 4095 || off >= (1ull << 36)) return -1;
+  for (uint32_t k = 0; k < n; k++)
+    if (U[off + k] >= 0x80) return -1;  // "replace"-decoded bytes: ranked on the host path
+  const uint64_t h = hash_str(U, off, n);
+  const uint64_t tag = (h >> 48) | 1;  // never 0 with off, n -- the empty slot is 0
+  const unsigned long long mine = (off << 28) | ((uint64_t)n << 16) | tag;
+  uint64_t slot = h & mask;
+  while (true) {
+    unsigned long long cur = __hip_atomic_load(&table[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == 0) {
+      const unsigned long long prev = atomicCAS(&table[slot], 0ull, mine);
+      if (prev == 0) return (int32_t)slot;
+      cur = prev;
+    }
+    if ((cur & 0xffff) == tag && ((cur >> 16) & 0xfff) == n && str_eq(U, cur >> 28, off, n)) return (int32_t)slot;
+    slot = (slot + 1) & mask;
+  }
+}
+
+// One lane per record: bamdec.cpp parse_record (same checks, same order of outcomes); any
+// record the host would reject or key differently sets *host.
+__global__ void k_parse(const uint8_t* __restrict__ U, const uint64_t* __restrict__ starts, uint64_t n,
+                        uint32_t is_cell, Cols C, Dicts D, uint32_t* __restrict__ flags) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint64_t p = starts[r];
+  const uint32_t bs = u32(U, p);
+  const uint64_t d = p + 4;
+  bool host = false;
+  do {
+    if (bs < 32) { host = true; break; }
+    const int32_t ref = (int32_t)u32(U, d), pos = (int32_t)u32(U, d + 4);
+    const uint32_t lrn = U[d + 8];
+    const uint32_t n_cigar = u16(U, d + 12), flag = u16(U, d + 14);
+    const uint32_t l_seq = u32(U, d + 16);
+    const uint64_t cig = d + 32 + lrn;
+    const uint64_t qual = cig + 4ull * n_cigar + (l_seq + 1ull) / 2;
+    const uint64_t tag0 = qual + l_seq;
+    const uint64_t end = d + bs;
+    if (tag0 > end) { host = true; break; }
+    DTag cb{}, cr{}, cy{}, ub{}, ur{}, uy{}, ge{}, xf{}, nh{};
+    uint64_t q = tag0;
+    while (q + 3 <= end) {
+      const uint32_t a = U[q], b = U[q + 1], t = U[q + 2];
+      q += 3;
+      DTag v{};
+      const uint32_t used = tag_value(U, q, end, t, &v);
+      if (!used) { host = true; break; }
+      q += used;
+      const uint32_t ab = a << 8 | b;
+      if (ab == ('C' << 8 | 'B')) cb = v;
+      else if (ab == ('C' << 8 | 'R')) cr = v;
+      else if (ab == ('C' << 8 | 'Y')) cy = v;
+      else if (ab == ('U' << 8 | 'B')) ub = v;
+      else if (ab == ('U' << 8 | 'R')) ur = v;
+      else if (ab == ('U' << 8 | 'Y')) uy = v;
+      else if (ab == ('G' << 8 | 'E')) ge = v;
+      else if (ab == ('X' << 8 | 'F')) xf = v;
+      else if (ab == ('N' << 8 | 'H')) nh = v;
+    }
+    if (host) break;
+    // dictionary values other than strings are keyed by the host path
+    if ((cb.kind && cb.kind != TV_STR) || (ub.kind && ub.kind != TV_STR) || (ge.kind && ge.kind != TV_STR)) {
+      host = true;
+      break;
+    }
+    bool validate = is_cell;
+    if (!is_cell) {
+      bool comma = false;
+      for (uint32_t k = 0; k < ge.n && ge.kind; k++) comma |= U[ge.off + k] == ',';
+      validate = !comma;
+    }
+    uint32_t bits = 0, cg = 0, cl = 0, ug = 0, ul = 0;
+    if (is_cell) {
+      if (cy.kind != TV_STR || cy.n == 0) { host = true; break; }
+      for (uint32_t k = 0; k < cy.n; k++) cg += U[cy.off + k] > 63;
+      cl = cy.n;
+      if (cb.kind) {
+        bits |= B_HAS_CB;
+        if (!cr.kind) { host = true; break; }
+        if (val_eq_str(U, cr, cb)) bits |= B_PERFECT_CB;
+      }
+    } else if (cb.kind) {
+      bits |= B_HAS_CB;
+    }
+    bool do_uy = validate;
+    if (!validate && uy.kind) {
+      if (uy.kind == TV_STR) do_uy = uy.n > 0;
+      else if (uy.kind == TV_INT && uy.i != 0) { host = true; break; }
+    }
+    if (do_uy) {
+      if (uy.kind != TV_STR || uy.n == 0) { host = true; break; }
+      for (uint32_t k = 0; k < uy.n; k++) ug += U[uy.off + k] > 63;
+      ul = uy.n;
+    }
+    if (ur.kind && ub.kind && val_eq_str(U, ur, ub)) bits |= B_PERFECT_UMI;
+    const bool aq_none = l_seq == 0 || U[qual] == 0xff;
+    uint32_t q0 = 0, q1 = 0;
+    if (!aq_none) {
+      uint32_t start = 0;
+      for (uint32_t k = 0; k < n_cigar; k++) {
+        const uint32_t c = u32(U, cig + 4ull * k), op = c & 0xf, len = c >> 4;
+        if (op == 5) {
+          if (start != 0 && start != l_seq) { host = true; break; }
+        } else if (op == 4) {
+          start += len;
+        } else {
+          break;
+        }
+      }
+      if (host) break;
+      uint32_t qend = l_seq;
+      for (int k = (int)n_cigar - 1; k > 0; k--) {
+        const uint32_t c = u32(U, cig + 4ull * k), op = c & 0xf, len = c >> 4;
+        if (op == 5) {
+          if (qend != l_seq) { host = true; break; }
+        } else if (op == 4) {
+          qend -= len;
+        } else {
+          break;
+        }
+      }
+      if (host) break;
+      q0 = start;
+      q1 = qend < start ? start : qend;
+    }
+    if (validate && (aq_none || q1 == q0)) { host = true; break; }
+    uint32_t x = XF_ABSENT;
+    if (xf.kind) {
+      x = XF_OTHER;
+      if (xf.kind == TV_STR) {
+        if (lit_eq(U, xf, "CODING", 6)) x = XF_CODING;
+        else if (lit_eq(U, xf, "INTRONIC", 8)) x = XF_INTRONIC;
+        else if (lit_eq(U, xf, "UTR", 3)) x = XF_UTR;
+        else if (lit_eq(U, xf, "INTERGENIC", 10)) x = XF_INTERGENIC;
+      }
+    }
+    if (flag & 0x4) {
+      bits |= B_UNMAPPED;
+    } else {
+      if (validate && (!xf.kind || !nh.kind)) { host = true; break; }
+      if (nh.kind == TV_INT && nh.i == 1) bits |= B_NH1;
+      uint64_t n_len = 0;
+      for (uint32_t k = 0; k < n_cigar; k++) {
+        const uint32_t c = u32(U, cig + 4ull * k);
+        if ((c & 0xf) == 3) n_len += c >> 4;
+      }
+      if (n_len) bits |= B_SPLICED;
+    }
+    if (flag & 0x10) bits |= B_REVERSE;
+    if (flag & 0x400) bits |= B_DUPLICATE;
+    uint32_t s = 0, g = 0;
+    for (uint32_t k = q0; k < q1; k++) {
+      const uint32_t v = U[qual + k];
+      s += v;
+      g += v > 30;
+    }
+    if (q1 - q0 > 0xffff || s > 0xffff || cl > 0xff || ul > 0xff) { host = true; break; }
+    int32_t id0 = -1, id1 = -1, id2 = -1;
+    if (cb.kind) host |= (id0 = intern(D.table[0], D.mask[0], U, cb.off, cb.n)) < 0;
+    else atomicOr(&flags[1], 1u);
+    if (ub.kind) host |= (id1 = intern(D.table[1], D.mask[1], U, ub.off, ub.n)) < 0;
+    else atomicOr(&flags[2], 1u);
+    if (ge.kind) host |= (id2 = intern(D.table[2], D.mask[2], U, ge.off, ge.n)) < 0;
+    else atomicOr(&flags[3], 1u);
+    if (host) break;
+    C.cell[r] = id0, C.umi[r] = id1, C.gene[r] = id2;
+    C.ref[r] = ref, C.pos[r] = pos;
+    C.gq_sum[r] = (uint16_t)s, C.gq_len[r] = (uint16_t)(q1 - q0), C.gq_gt30[r] = (uint16_t)g;
+    C.bits[r] = (uint8_t)bits, C.xf[r] = (uint8_t)x;
+    C.cy_gt30[r] = (uint8_t)cg, C.cy_len[r] = (uint8_t)cl, C.uy_gt30[r] = (uint8_t)ug, C.uy_len[r] = (uint8_t)ul;
+  } while (false);
+  if (host) atomicOr(&flags[0], 1u);
+}
+
+// ---------------- dictionaries ----------------
+__global__ void k_occupied(const unsigned long long* __restrict__ table, uint64_t cap, uint32_t* __restrict__ occ) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cap) occ[i] = table[i] != 0;
+}
+__global__ void k_compact(const unsigned long long* __restrict__ table, uint64_t cap,
+                          const uint32_t* __restrict__ dense, uint64_t* __restrict__ uoff,
+                          uint32_t* __restrict__ ulen) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  const unsigned long long v = table[i];
+  if (!v) return;
+  uoff[dense[i]] = v >> 28;
+  ulen[dense[i]] = (uint32_t)(v >> 16) & 0xfff;
+}
+__global__ void k_pack(const uint8_t* __restrict__ U, const uint64_t* __restrict__ uoff,
+                       const uint32_t* __restrict__ ulen, const uint64_t* __restrict__ boff, uint32_t n,
+                       uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t s = uoff[i], o = boff[i];
+  for (uint32_t k = 0; k < ulen[i]; k++) out[o + k] = U[s + k];
+}
+__global__ void k_remap(int32_t* __restrict__ col, uint64_t n, const uint32_t* __restrict__ dense,
+                        const int32_t* __restrict__ rank) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t v = col[i];
+  col[i] = v < 0 ? 0 : rank[dense[v]];
+}
+
+}  // namespace gb
+
+// ---------------- host ----------------
+namespace {
+using namespace gb;
+
+double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+thread_local std::string g_gerr;
+int gfail(int code, const char* msg) {
+  g_gerr = msg;
+  return code;
+}
+
+#define HIPOK(x)                                          \
+  do {                                                    \
+    hipError_t e_ = (x);                                  \
+    if (e_ != hipSuccess) return gfail(SCT_BAM_EIO, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t alloc(size_t count) {
+    free();
+    n = count;
+    return hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
+  }
+  void free() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DevBuf() { free(); }
+};
+
+// the byte offset where the alignments start: magic, l_text, text, n_ref, references
+// (SAM/BAM spec 4.2); the leading members are inflated on the host until it is known.
+// false: not a BAM header (the host path reports it).
+bool header_end(const uint8_t* f, const std::vector<Block>& blocks, uint64_t* H) {
+  std::vector<uint8_t> buf;
+  z_stream z;
+  memset(&z, 0, sizeof(z));
+  if (inflateInit2(&z, -15) != Z_OK) return false;
+  bool ok = false;
+  for (size_t k = 0; k < blocks.size(); k++) {
+    const size_t at = buf.size();
+    buf.resize(at + blocks[k].isize);
+    if (blocks[k].isize && !inflate_block(f, blocks[k], buf.data() + at, z)) break;
+    const size_t len = buf.size();
+    if (len < 12) continue;
+    if (memcmp(buf.data(), "BAM\1", 4) != 0) break;
+    uint64_t off = 8 + (uint64_t)rd32(buf.data() + 4);
+    if (off + 4 > len) continue;
+    const uint32_t n_ref = rd32(buf.data() + off);
+    off += 4;
+    bool done = true;
+    for (uint32_t r = 0; r < n_ref && done; r++) {
+      if (off + 4 > len) done = false;
+      else off += 4 + (uint64_t)rd32(buf.data() + off) + 4;
+    }
+    if (!done || off > len) continue;
+    *H = off;
+    ok = true;
+    break;
+  }
+  inflateEnd(&z);
+  return ok;
+}
+
+// Python's sorted() on the strings, the missing value first: rank of each distinct string
+void rank_strings(const std::string& bytes, const std::vector<uint64_t>& off, int32_t has_none,
+                  std::vector<int32_t>& rank, std::vector<uint32_t>& order) {
+  const size_t n = off.size() - 1;
+  order.resize(n);
+  for (size_t i = 0; i < n; i++) order[i] = (uint32_t)i;
+  auto sv = [&](uint32_t i) { return std::string_view(bytes.data() + off[i], off[i + 1] - off[i]); };
+  auto less = [&](uint32_t a, uint32_t b) { return sv(a) < sv(b); };
+  const size_t T = std::min<size_t>(16, std::max<size_t>(1, n / 65536));
+  if (T <= 1) {
+    std::sort(order.begin(), order.end(), less);
+  } else {  // sorted chunks, merged pairwise
+    std::vector<size_t> cut(T + 1);
+    for (size_t t = 0; t <= T; t++) cut[t] = n * t / T;
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < T; t++)
+      th.emplace_back([&, t] { std::sort(order.begin() + cut[t], order.begin() + cut[t + 1], less); });
+    for (auto& x : th) x.join();
+    for (size_t w = 1; w < T; w *= 2) {
+      th.clear();
+      for (size_t t = 0; t + w < T; t += 2 * w) {
+        const size_t a = cut[t], m = cut[t + w], b = cut[std::min(T, t + 2 * w)];
+        th.emplace_back([&, a, m, b] {
+          std::inplace_merge(order.begin() + a, order.begin() + m, order.begin() + b, less);
+        });
+      }
+      for (auto& x : th) x.join();
+    }
+  }
+  rank.resize(n);
+  for (size_t r = 0; r < n; r++) rank[order[r]] = (int32_t)r + has_none;
+}
+
+}  // namespace
+
+struct sct_gbam {
+  int device = 0;
+  hipStream_t st = nullptr;
+  DevBuf<uint8_t> in, u;
+  DevBuf<uint64_t> starts;
+  uint64_t ulen = 0, H = 0;
+  int64_t n = 0;
+  std::string dict_bytes[3];
+  std::vector<int64_t> dict_off[3];
+  int32_t has_none[3] = {0, 0, 0};
+  double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+
+namespace {
+
+template <class I, class O>
+hipError_t exclusive_sum(I* in, O* out, uint64_t n, hipStream_t st, DevBuf<uint8_t>& tmp) {
+  size_t bytes = 0;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n, st);
+  if (e != hipSuccess) return e;
+  if (tmp.n < bytes) {
+    e = tmp.alloc(bytes);
+    if (e != hipSuccess) return e;
+  }
+  return hipcub::DeviceScan::ExclusiveSum(tmp.p, bytes, in, out, (int)n, st);
+}
+
+inline unsigned grid(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+int open_impl(const char* path, int32_t device, void* stream, sct_gbam_t** out, int64_t* n_records) {
+  const double t0 = now();
+  std::unique_ptr<sct_gbam> G(new sct_gbam());
+  G->device = device;
+  G->st = (hipStream_t)stream;
+  HIPOK(hipSetDevice(device));
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return gfail(SCT_GBAM_HOST, "cannot open");
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || sb.st_size == 0) {
+    close(fd);
+    return gfail(SCT_GBAM_HOST, "empty file");
+  }
+  const uint64_t fsize = (uint64_t)sb.st_size;
+  const uint8_t* f = (const uint8_t*)mmap(nullptr, fsize, PROT_READ, MAP_PRIVATE, fd, 0);
+  close(fd);
+  if (f == MAP_FAILED) return gfail(SCT_GBAM_HOST, "cannot map");
+  struct Unmap {
+    const uint8_t* f;
+    uint64_t n;
+    ~Unmap() { munmap((void*)f, n); }
+  } unmap{f, fsize};
+  std::vector<Block> blocks;
+  if (scan_blocks(f, fsize, blocks) != SCT_BAM_OK) return gfail(SCT_GBAM_HOST, "not BGZF");
+  uint64_t H = 0;
+  if (!header_end(f, blocks, &H)) return gfail(SCT_GBAM_HOST, "no BAM header");
+  const uint32_t n_mem = (uint32_t)blocks.size();
+  std::vector<Member> mem(n_mem);
+  std::vector<uint64_t> O(n_mem + 1);
+  uint64_t ulen = 0;
+  for (uint32_t k = 0; k < n_mem; k++) {
+    const Block& b = blocks[k];
+    const uint16_t xlen = rd16(f + b.off + 10);
+    if (b.csize < 12u + xlen + 8u) return gfail(SCT_GBAM_HOST, "short member");
+    mem[k].in_off = b.off + 12 + xlen;
+    mem[k].clen = b.csize - 12 - xlen - 8;
+    mem[k].isize = b.isize;
+    mem[k].out_off = ulen;
+    O[k] = ulen;
+    ulen += b.isize;
+    if (b.isize > 65536) return gfail(SCT_GBAM_HOST, "member larger than 64 KB");
+  }
+  O[n_mem] = ulen;
+  G->ulen = ulen;
+  G->H = H;
+  if (H >= ulen) return gfail(SCT_GBAM_HOST, "no records");  // the host path's empty-file error
+  uint32_t mH = 0;
+  while (mH + 1 < n_mem && O[mH + 1] <= H) mH++;
+  G->t[0] = now() - t0;
+  G->t[6] = n_mem;
+
+  double t1 = now();
+  hipStream_t st = G->st;
+  HIPOK(G->in.alloc(fsize + kPad));
+  HIPOK(hipMemcpyAsync(G->in.p, f, fsize, hipMemcpyHostToDevice, st));
+  HIPOK(hipMemsetAsync(G->in.p + fsize, 0, kPad, st));
+  DevBuf<Member> d_mem;
+  DevBuf<uint64_t> d_O, d_S, d_land, d_base;
+  DevBuf<uint32_t> d_stat, d_cnt, d_flag;
+  HIPOK(d_mem.alloc(n_mem));
+  HIPOK(d_O.alloc(n_mem + 1));
+  HIPOK(hipMemcpyAsync(d_mem.p, mem.data(), n_mem * sizeof(Member), hipMemcpyHostToDevice, st));
+  HIPOK(hipMemcpyAsync(d_O.p, O.data(), (n_mem + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  HIPOK(hipStreamSynchronize(st));
+  G->t[1] = now() - t1;
+
+  t1 = now();
+  HIPOK(G->u.alloc(ulen + kPad));
+  HIPOK(hipMemsetAsync(G->u.p + ulen, 0, kPad, st));
+  HIPOK(d_stat.alloc(n_mem));
+  HIPOK(d_flag.alloc(4));
+  HIPOK(hipMemsetAsync(d_flag.p, 0, 4 * sizeof(uint32_t), st));
+  hipLaunchKernelGGL(k_inflate, dim3(n_mem), dim3(64), 0, st, G->in.p, d_mem.p, G->u.p, d_stat.p);
+  HIPOK(hipGetLastError());
+  hipLaunchKernelGGL(k_any, dim3(grid(n_mem, 256)), dim3(256), 0, st, d_stat.p, n_mem, d_flag.p);
+  uint32_t bad = 0;
+  HIPOK(hipMemcpyAsync(&bad, d_flag.p, sizeof(bad), hipMemcpyDeviceToHost, st));
+  HIPOK(hipStreamSynchronize(st));
+  G->t[2] = now() - t1;
+  if (bad) {
+    char msg[96];
+    snprintf(msg, sizeof(msg), "a BGZF member did not inflate on the device (status mask 0x%x)", bad);
+    return gfail(SCT_GBAM_HOST, msg);
+  }
+  G->in.free();
+
+  t1 = now();
+  HIPOK(d_S.alloc(n_mem + 1));
+  HIPOK(d_land.alloc(n_mem + 1));
+  HIPOK(d_cnt.alloc(n_mem));
+  HIPOK(d_base.alloc(n_mem + 1));
+  hipLaunchKernelGGL(k_guess, dim3(grid(n_mem, 64)), dim3(64), 0, st, G->u.p, ulen, d_O.p, mH, n_mem, H, d_S.p);
+  int rounds = 0;
+  for (;; rounds++) {
+    if (rounds == 64) return gfail(SCT_GBAM_HOST, "record starts did not converge");
+    hipLaunchKernelGGL(k_walk, dim3(grid(n_mem, 64)), dim3(64), 0, st, G->u.p, ulen, d_O.p, mH, n_mem, d_S.p,
+                       d_cnt.p, d_land.p, (uint64_t*)nullptr, (const uint64_t*)nullptr);
+    HIPOK(hipMemsetAsync(d_flag.p, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_fix, dim3(grid(n_mem + 1, 256)), dim3(256), 0, st, mH, n_mem, d_S.p, d_land.p, d_flag.p);
+    uint32_t nbad = 0;
+    HIPOK(hipMemcpyAsync(&nbad, d_flag.p, sizeof(nbad), hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    if (nbad == 0) break;
+    uint64_t lastland = 0;
+    HIPOK(hipMemcpy(&lastland, d_land.p + n_mem, sizeof(lastland), hipMemcpyDeviceToHost));
+    // only the final landing disagrees and every start before it is proven: a truncated record
+    if (nbad == 1 && lastland != ulen && rounds > 0) {
+      uint64_t s_last = 0;
+      HIPOK(hipMemcpy(&s_last, d_S.p + n_mem - 1, sizeof(s_last), hipMemcpyDeviceToHost));
+      if (s_last != kUnknown) return gfail(SCT_GBAM_HOST, "truncated BAM record");
+    }
+  }
+  G->t[7] = rounds;
+  DevBuf<uint8_t> tmp;
+  DevBuf<uint64_t> cnt64;
+  HIPOK(cnt64.alloc(n_mem + 1));
+  HIPOK(hipMemsetAsync(cnt64.p + n_mem, 0, sizeof(uint64_t), st));
+  hipLaunchKernelGGL(k_u32_to_u64, dim3(grid(n_mem, 256)), dim3(256), 0, st, d_cnt.p, cnt64.p, n_mem);
+  HIPOK(exclusive_sum(cnt64.p, d_base.p, n_mem + 1, st, tmp));
+  uint64_t n = 0;
+  HIPOK(hipMemcpyAsync(&n, d_base.p + n_mem, sizeof(n), hipMemcpyDeviceToHost, st));
+  HIPOK(hipStreamSynchronize(st));
+  if (n == 0) return gfail(SCT_GBAM_HOST, "no records");
+  HIPOK(G->starts.alloc(n));
+  hipLaunchKernelGGL(k_walk, dim3(grid(n_mem, 64)), dim3(64), 0, st, G->u.p, ulen, d_O.p, mH, n_mem, d_S.p,
+                     d_cnt.p, d_land.p, G->starts.p, (const uint64_t*)d_base.p);
+  HIPOK(hipStreamSynchronize(st));
+  G->t[3] = now() - t1;
+  G->n = (int64_t)n;
+  *n_records = (int64_t)n;
+  *out = G.release();
+  return SCT_BAM_OK;
+}
+
+int parse_impl(sct_gbam* G, int32_t metric_mode, void* const* cols) {
+  const double t0 = now();
+  HIPOK(hipSetDevice(G->device));
+  hipStream_t st = G->st;
+  const uint64_t n = (uint64_t)G->n;
+  uint64_t cap = 1024;
+  while (cap < 2 * n) cap <<= 1;
+  if (cap > (1ull << 31)) return gfail(SCT_GBAM_HOST, "too many records for the device tables");
+  DevBuf<unsigned long long> tab[3];
+  Dicts D;
+  for (int k = 0; k < 3; k++) {
+    HIPOK(tab[k].alloc(cap));
+    HIPOK(hipMemsetAsync(tab[k].p, 0, cap * sizeof(unsigned long long), st));
+    D.table[k] = tab[k].p;
+    D.mask[k] = cap - 1;
+  }
+  DevBuf<uint32_t> flags;
+  HIPOK(flags.alloc(4));
+  HIPOK(hipMemsetAsync(flags.p, 0, 4 * sizeof(uint32_t), st));
+  Cols C;
+  C.cell = (int32_t*)cols[0], C.umi = (int32_t*)cols[1], C.gene = (int32_t*)cols[2];
+  C.ref = (int32_t*)cols[3], C.pos = (int32_t*)cols[4];
+  C.gq_sum = (uint16_t*)cols[5], C.gq_len = (uint16_t*)cols[6], C.gq_gt30 = (uint16_t*)cols[7];
+  C.bits = (uint8_t*)cols[8], C.xf = (uint8_t*)cols[9], C.cy_gt30 = (uint8_t*)cols[10];
+  C.cy_len = (uint8_t*)cols[11], C.uy_gt30 = (uint8_t*)cols[12], C.uy_len = (uint8_t*)cols[13];
+  hipLaunchKernelGGL(k_parse, dim3(grid(n, 256)), dim3(256), 0, st, G->u.p, G->starts.p, n,
+                     metric_mode == SCT_BAM_CELL_METRICS ? 1u : 0u, C, D, flags.p);
+  HIPOK(hipGetLastError());
+  uint32_t fl[4];
+  HIPOK(hipMemcpyAsync(fl, flags.p, sizeof(fl), hipMemcpyDeviceToHost, st));
+  HIPOK(hipStreamSynchronize(st));
+  G->t[4] = now() - t0;
+  if (fl[0]) return gfail(SCT_GBAM_HOST, "a record needs the host decoder");
+
+  const double t1 = now();
+  DevBuf<uint32_t> occ, dense;
+  DevBuf<uint8_t> tmp;
+  HIPOK(occ.alloc(cap));
+  HIPOK(dense.alloc(cap));
+  int32_t* colk[3] = {C.cell, C.umi, C.gene};
+  for (int k = 0; k < 3; k++) {
+    const int32_t hn = fl[1 + k] ? 1 : 0;
+    G->has_none[k] = hn;
+    hipLaunchKernelGGL(k_occupied, dim3(grid(cap, 256)), dim3(256), 0, st, tab[k].p, cap, occ.p);
+    HIPOK(exclusive_sum(occ.p, dense.p, cap, st, tmp));
+    uint32_t last[2] = {0, 0};
+    HIPOK(hipMemcpyAsync(&last[0], dense.p + cap - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPOK(hipMemcpyAsync(&last[1], occ.p + cap - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    const uint64_t nu = (uint64_t)last[0] + last[1];
+    DevBuf<uint64_t> uoff, boff;
+    DevBuf<uint32_t> ulen;
+    DevBuf<int32_t> rank_d;
+    HIPOK(uoff.alloc(nu));
+    HIPOK(ulen.alloc(nu + 1));
+    HIPOK(boff.alloc(nu + 1));
+    HIPOK(hipMemsetAsync(ulen.p + nu, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_compact, dim3(grid(cap, 256)), dim3(256), 0, st, tab[k].p, cap, dense.p, uoff.p, ulen.p);
+    HIPOK(exclusive_sum(ulen.p, boff.p, nu + 1, st, tmp));
+    std::vector<uint64_t> hoff(nu + 1);
+    HIPOK(hipMemcpyAsync(hoff.data(), boff.p, (nu + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    const uint64_t total = hoff[nu];
+    DevBuf<uint8_t> packed;
+    HIPOK(packed.alloc(total));
+    if (nu)
+      hipLaunchKernelGGL(k_pack, dim3(grid(nu, 256)), dim3(256), 0, st, G->u.p, uoff.p, ulen.p, boff.p,
+                         (uint32_t)nu, packed.p);
+    std::string bytes(total, '\0');
+    if (total) HIPOK(hipMemcpyAsync(&bytes[0], packed.p, total, hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    std::vector<int32_t> rank;
+    std::vector<uint32_t> order;
+    rank_strings(bytes, hoff, hn, rank, order);
+    std::string& db = G->dict_bytes[k];
+    std::vector<int64_t>& dof = G->dict_off[k];
+    db.clear();
+    db.reserve(total);
+    dof.clear();
+    dof.reserve(nu + 2);
+    dof.push_back(0);
+    if (hn) dof.push_back(0);
+    for (uint64_t r = 0; r < nu; r++) {
+      const uint32_t i = order[r];
+      db.append(bytes.data() + hoff[i], hoff[i + 1] - hoff[i]);
+      dof.push_back((int64_t)db.size());
+    }
+    HIPOK(rank_d.alloc(nu));
+    if (nu) HIPOK(hipMemcpyAsync(rank_d.p, rank.data(), nu * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_remap, dim3(grid(n, 256)), dim3(256), 0, st, colk[k], n, dense.p, rank_d.p);
+    HIPOK(hipStreamSynchronize(st));
+  }
+  G->t[5] = now() - t1;
+  return SCT_BAM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sct_gbam_last_error(void) { return g_gerr.c_str(); }
+
+int sct_gbam_open(const char* path, int32_t device, void* stream, sct_gbam_t** out, int64_t* n_records) {
+  g_gerr.clear();
+  if (out) *out = nullptr;
+  if (n_records) *n_records = 0;
+  if (!path || !out || !n_records) return gfail(SCT_BAM_EIO, "NULL argument");
+  return open_impl(path, device, stream, out, n_records);
+}
+
+int sct_gbam_parse(sct_gbam_t* h, int32_t metric_mode, void* const* columns) {
+  g_gerr.clear();
+  if (!h || !columns) return gfail(SCT_BAM_EIO, "NULL argument");
+  if (metric_mode != SCT_BAM_CELL_METRICS && metric_mode != SCT_BAM_GENE_METRICS)
+    return gfail(SCT_BAM_EIO, "the device decode reads the cell and gene metric modes");
+  for (int k = 0; k < 14; k++)
+    if (!columns[k]) return gfail(SCT_BAM_EIO, "NULL column");
+  return parse_impl(h, metric_mode, columns);
+}
+
+int sct_gbam_dictionary(const sct_gbam_t* h, int32_t which, int64_t* n, const char** bytes, const int64_t** offsets,
+                        int32_t* has_none) {
+  if (!h || which < 0 || which > 2 || !n || !bytes || !offsets || !has_none) return gfail(SCT_BAM_EIO, "bad arguments");
+  *n = h->dict_off[which].empty() ? 0 : (int64_t)h->dict_off[which].size() - 1;
+  *bytes = h->dict_bytes[which].data();
+  *offsets = h->dict_off[which].data();
+  *has_none = h->has_none[which];
+  return SCT_BAM_OK;
+}
+
+int sct_gbam_read_inflated(const sct_gbam_t* h, uint64_t off, uint64_t n, void* dst, uint64_t* total) {
+  if (!h) return gfail(SCT_BAM_EIO, "NULL handle");
+  if (total) *total = h->ulen;
+  if (!n) return SCT_BAM_OK;
+  if (!dst || off > h->ulen || n > h->ulen - off) return gfail(SCT_BAM_EIO, "range outside the payload");
+  HIPOK(hipSetDevice(h->device));
+  HIPOK(hipMemcpy(dst, h->u.p + off, n, hipMemcpyDeviceToHost));
+  return SCT_BAM_OK;
+}
+
+int sct_gbam_timing(const sct_gbam_t* h, double* t8) {
+  if (!h || !t8) return gfail(SCT_BAM_EIO, "NULL argument");
+  for (int k = 0; k < 8; k++) t8[k] = h->t[k];
+  return SCT_BAM_OK;
+}
+
+void sct_gbam_close(sct_gbam_t* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  delete h;
+}
+
+}  // extern "C"

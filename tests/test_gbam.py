@@ -1,0 +1,163 @@
+"""Device BAM decode (libsct_gbam.so, include/sct_gbam.h) against zlib and the host decoder.
+
+The inflated payload must equal zlib's byte for byte, and the columns and dictionaries must equal
+libsct_bam.so's (itself checked against the pure-Python decoder in test_bam_native.py) for every
+bundled BAM, for the same payloads re-blocked with other deflate settings (stored, fixed-code,
+Huffman-only and RLE blocks, many blocks per member, members cutting records anywhere), and
+for files the device path must decline (records the reference rejects, typed dictionary tags):
+there ``decode`` returns None and the host decoder raises as the reference does.
+"""
+import os
+import re
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import helpers as H
+from sctools_amd import bamnative, gbam
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(H.GOLDEN, "bam")
+BAMS = sorted(f[:-4] for f in os.listdir(GOLD) if f.endswith(".bam"))
+
+
+def test_every_declared_symbol_is_exported():
+    text = open(os.path.join(ROOT, "include", "sct_gbam.h")).read()
+    names = sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(sct_\w+)\(", text, flags=re.M)))
+    assert set(names) == set(gbam.EXPORTED)
+    lib = gbam.load()
+    for name in names:
+        assert hasattr(lib, name), name
+
+
+def members(data: bytes):
+    off = 0
+    while off < len(data):
+        xlen = struct.unpack_from("<H", data, off + 10)[0]
+        bsize = struct.unpack_from("<H", data, off + 12 + xlen - 2)[0] + 1
+        yield data[off + 12 + xlen: off + bsize - 8]
+        off += bsize
+
+
+def payload(path) -> bytes:
+    data = open(path, "rb").read()
+    return b"".join(zlib.decompress(m, -15) for m in members(data))
+
+
+def rebgzf(raw: bytes, path, level=6, strategy=zlib.Z_DEFAULT_STRATEGY, block=65280, mem_level=8):
+    """raw payload -> BGZF with the given deflate settings (htslib's layout, then the EOF member)."""
+    with open(path, "wb") as f:
+        for i in range(0, len(raw), block):
+            chunk = raw[i:i + block]
+            c = zlib.compressobj(level, zlib.DEFLATED, -15, mem_level, strategy)
+            comp = c.compress(chunk) + c.flush()
+            head = struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, len(comp) + 25)
+            f.write(head + comp + struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk)))
+        f.write(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+
+
+def host(path, mode):
+    try:
+        return bamnative.decode(path, mode)
+    except Exception as e:  # noqa: BLE001 -- the reference's exception for this file
+        return e
+
+
+def same_as_host(path, mode):
+    want = host(path, mode)
+    got = gbam.decode(path, mode)
+    if isinstance(want, Exception):
+        assert got is None, (path, mode, want)
+        return None
+    assert got is not None, (path, mode, gbam.last_error())
+    cols, names = got
+    arrays, want_names = want
+    assert names == want_names
+    for c, a in arrays.items():
+        g = cols[c].cpu().numpy().view(a.dtype)
+        assert np.array_equal(g, a), (path, mode, c)
+    return cols
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bam", BAMS)
+def test_inflate_matches_zlib(bam):
+    path = os.path.join(GOLD, bam + ".bam")
+    got = gbam.inflate(path)
+    assert got is not None, gbam.last_error()
+    assert got == payload(path)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bam", BAMS)
+@pytest.mark.parametrize("mode", ["cell", "gene"])
+def test_columns_match_host_decoder(bam, mode):
+    same_as_host(os.path.join(GOLD, bam + ".bam"), mode)
+
+
+SETTINGS = [
+    dict(level=0),  # stored blocks
+    dict(level=1),
+    dict(level=9),
+    dict(level=6, strategy=zlib.Z_FIXED),
+    dict(level=6, strategy=zlib.Z_HUFFMAN_ONLY),
+    dict(level=6, strategy=zlib.Z_RLE),
+    dict(level=6, mem_level=1),  # many small deflate blocks per member
+    dict(level=6, block=997),  # members cut records anywhere; many records span members
+    dict(level=6, block=65536),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("setting", SETTINGS, ids=lambda s: "-".join("%s%s" % kv for kv in s.items()))
+def test_reblocked_payloads(tmp_path, setting):
+    raw = payload(os.path.join(GOLD, "small-cell-sorted.bam"))
+    path = str(tmp_path / "re.bam")
+    rebgzf(raw, path, **setting)
+    assert gbam.inflate(path) == raw
+    same_as_host(path, "cell")
+    same_as_host(path, "gene")
+
+
+@pytest.mark.gpu
+def test_many_members_and_records(tmp_path):
+    """~60k records over ~300 members: every record start found, every string interned."""
+    raw = payload(os.path.join(GOLD, "small-cell-sorted.bam"))
+    hdr_end = _header_end(raw)
+    body = raw[hdr_end:]
+    reps = []
+    for r in range(90):  # the first CB character per replica: same lengths, new barcodes
+        reps.append(re.sub(rb"CBZ.", b"CBZ" + bytes([65 + r % 26]), body))
+    big = raw[:hdr_end] + b"".join(reps)
+    path = str(tmp_path / "big.bam")
+    rebgzf(big, path, level=6, block=65280)
+    assert gbam.inflate(path) == big
+    cols = same_as_host(path, "cell")
+    assert cols is not None and cols["cell"].numel() > 50000
+
+
+def _header_end(raw: bytes) -> int:
+    off = 8 + struct.unpack_from("<i", raw, 4)[0]
+    n_ref = struct.unpack_from("<i", raw, off)[0]
+    off += 4
+    for _ in range(n_ref):
+        off += 4 + struct.unpack_from("<i", raw, off)[0] + 4
+    return off
+
+
+@pytest.mark.gpu
+def test_corrupt_member_declines(tmp_path):
+    raw = payload(os.path.join(GOLD, "small-cell-sorted.bam"))
+    path = str(tmp_path / "bad.bam")
+    rebgzf(raw, path, level=6)
+    data = bytearray(open(path, "rb").read())
+    data[60] ^= 0xFF  # inside the first member's deflate data
+    open(path, "wb").write(bytes(data))
+    try:
+        payload(path)
+    except zlib.error:
+        assert gbam.decode(path, "cell") is None
+        return
+    same_as_host(path, "cell")  # the flip left a valid stream: both decoders read the same bytes
