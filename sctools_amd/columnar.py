@@ -89,8 +89,39 @@ class Dictionary:
         return np.fromiter((idx[v] for v in values), dtype=np.int32, count=len(values))
 
 
+class PackedDictionary:
+    """A ranked dictionary as the decoders hand it over: the names' bytes back to back in id
+    order, their offsets, and whether id 0 is the missing tag.  Names are decoded to ``str`` only
+    when asked for (a UMI dictionary of millions of entries is needed only for its length)."""
+
+    def __init__(self, raw: bytes, offsets: np.ndarray, has_none: bool):
+        self._raw, self._off, self._has_none = raw, offsets, bool(has_none)
+        self._names: Optional[List] = None
+        self._index: Optional[Dict] = None
+
+    def __len__(self):
+        return len(self._off) - 1
+
+    @property
+    def names(self) -> List:
+        if self._names is None:
+            raw, off = self._raw, self._off.tolist()
+            lst = [raw[off[i]:off[i + 1]].decode("utf-8") for i in range(len(off) - 1)]
+            if self._has_none:
+                lst[0] = None
+            self._names = lst
+        return self._names
+
+    @property
+    def index(self) -> Dict:
+        if self._index is None:
+            self._index = {v: i for i, v in enumerate(self.names)}
+        return self._index
+
+
 class Columns:
-    """Columnar records plus the dictionaries needed to print entity names."""
+    """Columnar records plus the dictionaries needed to print entity names.  ``arrays`` holds
+    numpy columns (host decode) or device tensors (``gbam``, decoded on the GPU)."""
 
     def __init__(self, arrays: Dict[str, np.ndarray], cells: Dictionary, umis: Dictionary,
                  genes: Dictionary):
@@ -102,6 +133,30 @@ class Columns:
     @property
     def n(self) -> int:
         return int(self.arrays["cell"].shape[0])
+
+    @property
+    def on_device(self) -> bool:
+        return not isinstance(self.arrays["cell"], np.ndarray)
+
+    def host(self) -> "Columns":
+        """These columns with numpy arrays (copied from the device when they live there)."""
+        if not self.on_device:
+            return self
+        arrays = {}
+        for c, t in self.arrays.items():
+            a = t.cpu().numpy()
+            arrays[c] = a.view(np.uint16) if a.dtype == np.int16 else a
+        return Columns(arrays, self.cells, self.umis, self.genes)
+
+    def column_at(self, name: str, index: np.ndarray) -> np.ndarray:
+        """``arrays[name][index]`` as numpy, gathered on the device for device columns."""
+        a = self.arrays[name]
+        if isinstance(a, np.ndarray):
+            return a[index]
+        import torch
+
+        idx = torch.from_numpy(np.ascontiguousarray(index, dtype=np.int64)).to(a.device)
+        return a[idx].cpu().numpy()
 
     def gene_flags(self, mitochondrial_gene_ids=frozenset()):
         """(is_mito, is_multi) uint8 per gene id.
@@ -215,7 +270,8 @@ def build_columns(cell_v: List, umi_v: List, gene_v: List, numeric: List[tuple])
     return Columns(arrays, cells, umis, genes)
 
 
-def columnarize(path: str, mode: str = "rb", metric_mode: str = MODE_CELL, native: Optional[bool] = None) -> Columns:
+def columnarize(path: str, mode: str = "rb", metric_mode: str = MODE_CELL, native: Optional[bool] = None,
+                device=None) -> Columns:
     """Decode ``path`` into :class:`Columns`, validating like the reference.
 
     ``metric_mode`` selects which tags are required: ``cell`` also needs
@@ -223,11 +279,21 @@ def columnarize(path: str, mode: str = "rb", metric_mode: str = MODE_CELL, nativ
     does; ``gene`` does not, and records of multi-gene GE runs are never
     validated because ``GatherGeneMetrics`` skips them (``gatherer.py:210-212``).
 
-    BAM input goes through the native decoder (``libsct_bam.so``, all cores) unless
-    ``native=False``; SAM text, and BAM with ``native=False``, through the Python reader.
+    With ``device`` (a torch device) a BAM is decoded on that GPU (``gbam``: inflate, record
+    starts, parse and interning in HBM) and the columns stay there.  A file the device path
+    declines (a record the reference rejects, typed dictionary tags) and every other case go
+    through the native host decoder (``libsct_bam.so``, all cores) unless ``native=False``;
+    SAM text, and BAM with ``native=False``, through the Python reader.
     """
     from sctools_amd import bamnative
 
+    if device is not None and mode == "rb" and native is not False:
+        from sctools_amd import gbam
+
+        got = gbam.decode(path, metric_mode, device, lazy=True)
+        if got is not None:
+            arrays, (cn, un, gn) = got
+            return Columns(arrays, cn, un, gn)
     if native is None:
         native = mode == "rb" and bamnative.available()
     if native:

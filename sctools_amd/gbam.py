@@ -96,9 +96,11 @@ def _check(rc: int):
         raise OSError("device BAM decode failed (%d): %s" % (rc, last_error()))
 
 
-def decode(path: str, metric_mode: str = "cell", device=None, timings: Optional[dict] = None):
+def decode(path: str, metric_mode: str = "cell", device=None, timings: Optional[dict] = None,
+           lazy: bool = False):
     """(device column tensors, [cell names, umi names, gene names]) -- or None when the file needs
-    the host decoder.  Names in id order, None first when a record lacks the tag."""
+    the host decoder.  Names in id order, None first when a record lacks the tag; with ``lazy``
+    each dictionary is a ``columnar.PackedDictionary`` (strings decoded only when asked for)."""
     import torch
 
     from sctools_amd import _native as N
@@ -124,6 +126,11 @@ def decode(path: str, metric_mode: str = "cell", device=None, timings: Optional[
             offs = np.frombuffer((ctypes.c_int64 * (k + 1)).from_address(off.value), dtype=np.int64).copy()
             total = int(offs[-1])
             raw = ctypes.string_at(by.value, total) if total else b""
+            if lazy:
+                from sctools_amd.columnar import PackedDictionary
+
+                names.append(PackedDictionary(raw, offs, bool(hn.value)))
+                continue
             lst = [raw[offs[i]:offs[i + 1]].decode("utf-8") for i in range(k)]
             if hn.value:
                 lst[0] = None

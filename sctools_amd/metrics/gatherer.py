@@ -8,10 +8,11 @@ read a BAM ('rb') or SAM ('r'), aggregate per cell-barcode run
 runs skipped), write ``output_stem.csv.gz`` (or ``.csv``) with the reference's
 header and row format.
 
-The per-record aggregation runs on the GPU (``sctools_amd.engine``): the host
-decodes the file into columns (``sctools_amd.columnar``), raising the same
-exception types the reference raises, and the HIP engine computes every row
-in one launch sequence.  ``float_mode='welford'`` (default) reproduces the
+The per-record aggregation runs on the GPU (``sctools_amd.engine``): a BAM is
+inflated and parsed into columns on the same GPU (``sctools_amd.gbam``; a file
+it declines -- one the reference rejects -- is decoded on the host by
+``sctools_amd.columnar``, raising the same exception types the reference
+raises), and the HIP engine computes every row in one launch sequence.  ``float_mode='welford'`` (default) reproduces the
 reference's sequential Welford floats bit for bit; ``'exact'`` computes
 correctly rounded mean / variance from exact sums (order independent,
 within 1e-12 of Welford).
@@ -48,7 +49,10 @@ def compute_rows(cols: columnar.Columns, mode: str, mitochondrial_gene_ids=froze
         return multigpu.compute_rows(cols, mode, mitochondrial_gene_ids, float_mode, devices)
 
     eng = E.get_engine(device)
-    dev_cols = E.to_device(cols.arrays, eng.device)
+    if cols.on_device:
+        dev_cols = cols.arrays
+    else:
+        dev_cols = E.to_device(cols.arrays, eng.device)
     mito, multi = cols.gene_flags(mitochondrial_gene_ids)
     dims = E.Dims(len(cols.cells), len(cols.genes), len(cols.umis))
     gm = torch.from_numpy(mito).to(eng.device)
@@ -59,9 +63,9 @@ def compute_rows(cols: columnar.Columns, mode: str, mitochondrial_gene_ids=froze
 
 def write_rows(writer: MetricCSVWriter, mode: str, cols: columnar.Columns, ints: np.ndarray,
                floats: np.ndarray) -> None:
-    key = cols.arrays["cell" if mode == "cell" else "gene"]
+    ids = cols.column_at("cell" if mode == "cell" else "gene", ints[:, N.I_ENTITY])
     names_of = cols.cells.names if mode == "cell" else cols.genes.names
-    names = [names_of[key[i]] for i in ints[:, N.I_ENTITY]]
+    names = [names_of[i] for i in ids.tolist()]
     keep, kept = R.select_rows(mode, ints, names)
     writer.write_bytes(R.format_rows_bytes(mode, kept, ints[keep], floats[keep]))
 
@@ -71,7 +75,7 @@ class MetricGatherer:
 
     def __init__(self, bam_file: str, output_stem: str, mitochondrial_gene_ids: Set[str] = set(),
                  compress: bool = True, float_mode: str = "welford", device: Optional[str] = None,
-                 devices=None):
+                 devices=None, gpu_decode: bool = True):
         self._bam_file = bam_file
         self._output_stem = output_stem
         self._compress = compress
@@ -79,6 +83,20 @@ class MetricGatherer:
         self._float_mode = float_mode
         self._device = device
         self._devices = devices  # None: one device (`device`); int N or device list: multigpu
+        self._gpu_decode = gpu_decode  # one device: inflate and parse a BAM on it (gbam)
+
+    def _columns(self, mode: str, metric_mode: str) -> columnar.Columns:
+        """The file's columns: decoded on the GPU that computes the metrics when there is one
+        device and the input is BAM (a file the device decoder declines goes through the host
+        decoder, which raises the reference's exception), else on the host."""
+        if self._devices is None and self._gpu_decode and mode == "rb":
+            from sctools_amd import engine as E
+            from sctools_amd import gbam
+
+            if gbam.available():
+                dev = E.get_engine(self._device).device
+                return columnar.columnarize(self.bam_file, mode, metric_mode, device=dev)
+        return columnar.columnarize(self.bam_file, mode, metric_mode)
 
     @property
     def bam_file(self) -> str:
@@ -95,7 +113,7 @@ class GatherCellMetrics(MetricGatherer):
     def extract_metrics(self, mode: str = "rb") -> None:
         with MetricCSVWriter(self._output_stem, self._compress) as out:
             out.write_header(vars(CellMetrics()))
-            cols = columnar.columnarize(self.bam_file, mode, columnar.MODE_CELL)
+            cols = self._columns(mode, columnar.MODE_CELL)
             ints, floats = compute_rows(cols, "cell", self._mitochondrial_gene_ids, self._float_mode,
                                         self._device, self._devices)
             write_rows(out, "cell", cols, ints, floats)
@@ -107,7 +125,7 @@ class GatherGeneMetrics(MetricGatherer):
     def extract_metrics(self, mode: str = "rb") -> None:
         with MetricCSVWriter(self._output_stem, self._compress) as out:
             out.write_header(vars(GeneMetrics()))
-            cols = columnar.columnarize(self.bam_file, mode, columnar.MODE_GENE)
+            cols = self._columns(mode, columnar.MODE_GENE)
             ints, floats = compute_rows(cols, "gene", frozenset(), self._float_mode, self._device,
                                         self._devices)
             write_rows(out, "gene", cols, ints, floats)

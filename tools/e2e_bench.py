@@ -1,74 +1,174 @@
-"""End-to-end drop-in timing: GatherCellMetrics / GatherGeneMetrics on a BAM (decode -> GPU -> CSV.gz).
+"""End-to-end drop-in timing: GatherCellMetrics on a BAM (decode -> GPU metrics -> CSV.gz).
 
-python tools/e2e_bench.py [--replicas R] [--bam PATH]   (needs a GPU)
+python tools/e2e_bench.py [--records N] [--bam PATH] [--host-decoder]   (needs a GPU)
 
-The BAM is the reference's small-cell-sorted.bam fixture replicated R times, each replica with
-its own cell barcodes (CB + '-r'), written once with tests/bamwriter.py.  Prints one JSON line:
-records, seconds per stage (native decode, H2D + GPU metrics, CSV text + gzip) and records/s.
+The BAM is the reference's small-cell-sorted.bam payload (656 records of 58 cells) replicated
+until it holds N records, every group of --replicas-per-cell consecutive replicas given one cell
+barcode of its own (CB and CR rewritten in place, same length), so cells hold ~2.6k records as in
+a 10x v2 run rather than the fixture's ~11 (UB / UR prefixes vary per replica too).  It is written once (BGZF, zlib level 6, 0xff00-byte
+members as htslib writes them, compressed by a process pool).  Prints one JSON line: records,
+seconds per stage -- the device decode's own stages (map + scan, copy, inflate, record starts,
+parse + intern, dictionaries), GPU metrics, CSV text + gzip -- and records/s end to end, for
+``GatherCellMetrics(bam).extract_metrics()`` (the drop-in) timed as one call, plus the same call
+with the host decoder when --host-decoder is given.
 """
 import argparse
 import json
 import os
+import re
+import struct
 import sys
 import time
+import zlib
+from multiprocessing import Pool
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tests"))
+FIXTURE = os.path.join(ROOT, "tests", "golden", "bam", "small-cell-sorted.bam")
+EOF_MEMBER = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+BLOCK = 0xff00
 
 
-def make_bam(path, replicas):
-    import bamwriter
-    from sctools_amd.bam import open_alignments
+def _payload(path):
+    data = open(path, "rb").read()
+    out, off = [], 0
+    while off < len(data):
+        xlen = struct.unpack_from("<H", data, off + 10)[0]
+        bsize = struct.unpack_from("<H", data, off + 12 + xlen - 2)[0] + 1
+        out.append(zlib.decompress(data[off + 12 + xlen: off + bsize - 8], -15))
+        off += bsize
+    return b"".join(out)
 
-    base = list(open_alignments(os.path.join(ROOT, "tests", "golden", "bam", "small-cell-sorted.bam"), "rb"))
+
+def _header_end(raw):
+    off = 8 + struct.unpack_from("<i", raw, 4)[0]
+    n_ref = struct.unpack_from("<i", raw, off)[0]
+    off += 4
+    for _ in range(n_ref):
+        off += 4 + struct.unpack_from("<i", raw, off)[0] + 4
+    return off
+
+
+def _bgzf(raw):
     out = []
-    for r in range(replicas):
-        for rec in base:
-            t = dict(rec._tags)
-            if "CB" in t:
-                t["CB"] = "%s-%d" % (t["CB"], r)
-                t["CR"] = t["CB"] if rec._tags.get("CR") == rec._tags.get("CB") else t.get("CR")
-            x = type(rec)(rec.query_name, rec.flag, rec.reference_id, rec.pos, rec.mapq, rec.cigar, rec.l_seq,
-                          rec._qual, t)
-            out.append(x)
-    bamwriter.write_bam(path, out)
+    for i in range(0, len(raw), BLOCK):
+        chunk = raw[i:i + BLOCK]
+        c = zlib.compressobj(6, zlib.DEFLATED, -15)
+        comp = c.compress(chunk) + c.flush()
+        head = struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, len(comp) + 25)
+        out.append(head + comp + struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk)))
+    return b"".join(out)
+
+
+_BODY = None
+
+
+def _init(body):
+    global _BODY
+    _BODY = body
+
+
+def _group(args):
+    """Compressed members of replicas [lo, hi): replica r's CB / CR values become cell r // k, and
+    the first 5 bases of its UB / UR values encode r % 1024 (more molecule barcodes)."""
+    lo, hi, k = args
+    parts = []
+    for r in range(lo, hi):
+        bc = b"%016d" % (r // k)
+        u = bytes(b"ACGT"[(r % 1024) >> (2 * i) & 3] for i in range(5))
+        b = re.sub(rb"CBZ[^\x00]{16}\x00", b"CBZ" + bc + b"\x00", _BODY)
+        b = re.sub(rb"CRZ[^\x00]{16}\x00", b"CRZ" + bc + b"\x00", b)
+        b = re.sub(rb"UBZ[^\x00]{5}", b"UBZ" + u, b)
+        parts.append(re.sub(rb"URZ[^\x00]{5}", b"URZ" + u, b))
+    return _bgzf(b"".join(parts))
+
+
+def make_bam(path, records, per_cell, procs=16):
+    raw = _payload(FIXTURE)
+    h = _header_end(raw)
+    body = raw[h:]
+    n_body = body.count(b"CBZ")  # every fixture record carries CB
+    reps = (records + n_body - 1) // n_body
+    step = 64
+    jobs = [(lo, min(reps, lo + step), per_cell) for lo in range(0, reps, step)]
+    with open(path + ".tmp", "wb") as f:
+        f.write(_bgzf(raw[:h]))
+        with Pool(procs, initializer=_init, initargs=(body,)) as pool:
+            for blob in pool.imap(_group, jobs):
+                f.write(blob)
+        f.write(EOF_MEMBER)
+    os.replace(path + ".tmp", path)
+    return reps * n_body
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--replicas", type=int, default=3000)
-    ap.add_argument("--bam", default="/tmp/sct_e2e.bam")
+    ap.add_argument("--records", type=int, default=24_000_000)
+    ap.add_argument("--replicas-per-cell", type=int, default=4)
+    ap.add_argument("--bam", default=None)
+    ap.add_argument("--host-decoder", action="store_true")
+    ap.add_argument("--float-mode", default="welford")
     a = ap.parse_args()
-    if not os.path.exists(a.bam):
+    bam = a.bam or "/tmp/sct_e2e_%d.bam" % a.records
+    if not os.path.exists(bam):
         t0 = time.time()
-        make_bam(a.bam, a.replicas)
-        print("wrote %s in %.1fs" % (a.bam, time.time() - t0), file=sys.stderr, flush=True)
+        n = make_bam(bam, a.records, a.replicas_per_cell)
+        print("wrote %s (%d records, %.0f MB) in %.1fs" % (bam, n, os.path.getsize(bam) / 1e6, time.time() - t0),
+              file=sys.stderr, flush=True)
     import torch
 
-    from sctools_amd import columnar
+    from sctools_amd import columnar, gbam
     from sctools_amd.metrics import gatherer as G
-    from sctools_amd.metrics.writer import MetricCSVWriter
     from sctools_amd.metrics.aggregator import CellMetrics
+    from sctools_amd.metrics.writer import MetricCSVWriter
 
     torch.cuda.init()
-    res = {"bam": a.bam, "bam_mb": os.path.getsize(a.bam) / 1e6}
-    G.compute_rows(columnar.columnarize(a.bam, "rb", "cell"), "cell", float_mode="exact")  # warm-up
+    dev = torch.device("cuda", 0)
+    res = {"bam": bam, "bam_mb": os.path.getsize(bam) / 1e6, "float_mode": a.float_mode}
+    with open(bam, "rb") as f:  # page cache warm: the timed runs read memory, not the disk
+        while f.read(1 << 26):
+            pass
+    G.GatherCellMetrics(bam, "/tmp/sct_e2e_warm", float_mode=a.float_mode).extract_metrics()  # warm-up
     torch.cuda.synchronize()
+
+    # stage breakdown of the device path
+    tm = {}
     t0 = time.perf_counter()
-    cols = columnar.columnarize(a.bam, "rb", "cell")
+    got = gbam.decode(bam, "cell", dev, timings=tm, lazy=True)
+    torch.cuda.synchronize()
     t1 = time.perf_counter()
-    ints, floats = G.compute_rows(cols, "cell", float_mode="welford")
+    if got is None:
+        raise SystemExit("the device decoder declined %s: %s" % (bam, gbam.last_error()))
+    arrays, (cn, un, gn) = got
+    cols = columnar.Columns(arrays, cn, un, gn)
+    ints, floats = G.compute_rows(cols, "cell", float_mode=a.float_mode, device=dev)
     t2 = time.perf_counter()
     with MetricCSVWriter("/tmp/sct_e2e_cell", compress=True) as w:
         w.write_header(vars(CellMetrics()))
         G.write_rows(w, "cell", cols, ints, floats)
     t3 = time.perf_counter()
-    res.update({"records": cols.n, "cells": int(ints.shape[0]), "decode_s": t1 - t0, "gpu_metrics_s": t2 - t1,
+    res.update({"records": cols.n, "cells": int(ints.shape[0]), "umis": len(un), "genes": len(gn),
+                "device_decode_s": t1 - t0, "device_decode_stages_s": tm, "gpu_metrics_s": t2 - t1,
                 "csv_gz_s": t3 - t2, "total_s": t3 - t0, "records_per_s": cols.n / (t3 - t0)})
-    t0 = time.perf_counter()
-    G.GatherCellMetrics(a.bam, "/tmp/sct_e2e_cell2").extract_metrics()
-    res["GatherCellMetrics_s"] = time.perf_counter() - t0
+    del cols, arrays, got
+    torch.cuda.empty_cache()
+
+    runs = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        G.GatherCellMetrics(bam, "/tmp/sct_e2e_cell2", float_mode=a.float_mode).extract_metrics()
+        runs.append(time.perf_counter() - t0)
+    res["GatherCellMetrics_s"] = runs
+    res["GatherCellMetrics_records_per_s"] = res["records"] / min(runs)
+    if a.host_decoder:
+        t0 = time.perf_counter()
+        G.GatherCellMetrics(bam, "/tmp/sct_e2e_cell3", float_mode=a.float_mode, gpu_decode=False).extract_metrics()
+        res["GatherCellMetrics_host_decoder_s"] = time.perf_counter() - t0
+        res["GatherCellMetrics_host_decoder_records_per_s"] = res["records"] / res["GatherCellMetrics_host_decoder_s"]
+        import gzip
+
+        same = gzip.open("/tmp/sct_e2e_cell2.csv.gz").read() == gzip.open("/tmp/sct_e2e_cell3.csv.gz").read()
+        res["device_and_host_decoder_csv_identical"] = same
     print(json.dumps(res))
 
 
