@@ -155,8 +155,11 @@ __device__ __forceinline__ void welford_store(double* F, int st, double mean, do
   F[vslot] = var;
 }
 
-// The stream values of every record, once, in parallel: xs[st * n + i] = x[st] of record i
-// (welford_samples); the chains below then load one double per record.
+// The stream values of every record, once, in parallel: xs[4 i + st] = x[st] of record i
+// (welford_samples), a record's four streams side by side, so the 4 chain lanes of one entity load
+// 32 contiguous bytes (a wave's load touches 16 lines, not 64).  The chains below load one double
+// per record; xs holds kWfPad records of slack past n for their unclamped reads.
+constexpr int kWfPad = 64;
 template <bool kCell>
 __global__ void __launch_bounds__(kBlock) k_welford_x(RecCols r, int64_t n, double* __restrict__ xs) {
   __shared__ double s_rcp[kRcpN];
@@ -166,31 +169,39 @@ __global__ void __launch_bounds__(kBlock) k_welford_x(RecCols r, int64_t n, doub
   if (i >= n) return;
   double x[4];
   welford_samples<kCell>(r, i, s_rcp, x);
-#pragma unroll
-  for (int st = 0; st < (kCell ? 4 : 3); st++) xs[st * n + i] = x[st];
+  double2* o = reinterpret_cast<double2*>(xs + 4 * i);
+  o[0] = make_double2(x[0], x[1]);
+  o[1] = make_double2(x[2], kCell ? x[3] : 0.0);
 }
 
 // Big entities: one lane per (entity, stream) chain, kWfGroup entities x 4 streams per wave, groups
 // of similar sizes (the order is by descending log2 size), waves dequeue groups.  Every lane steps
 // the same record index k together, so RN(1 / k) is the same for all of them: the wave computes 64
-// of them at a time into LDS (one division per lane per 64 records).  Per record a lane loads its
-// sample (kWfBatch records per batch; the next batch's loads, unconditional with clamped addresses,
-// are in flight while this batch's kWfBatch updates run: enough work to cover HBM latency) and runs
-// the update: the chain is 5 dependent FP64 operations, and nothing on it waits for memory.
+// of them at a time, one per lane in registers (one division per lane per 64 records), and record
+// q's pair reaches the chain by readlane (reading it from LDS put the LDS latency on the chain every
+// few records: 22 ms at config 2).  Per record a lane loads its sample (kWfBatch records per batch;
+// the next batch's loads, unconditional with clamped addresses, are in flight while this batch's
+// kWfBatch updates run) and runs the update: 4 dependent FP64 operations, nothing on them waiting
+// for memory or LDS.
 constexpr int kWfGroup = kWave / 4;
 constexpr int kWfBatch = 32;
 static_assert(kWave % kWfBatch == 0, "batches tile the 64-record y chunks");
 constexpr int kWfBlocks = 2048;  // persistent grid (waves dequeue groups)
+// lane l's double, broadcast (l a compile-time constant after unrolling)
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 template <bool kCell>
 __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __restrict__ ent_start, int64_t n_ent,
                                                            int64_t n, const uint32_t* __restrict__ order,
                                                            WelfordCtl* __restrict__ ctl,
                                                            const double* __restrict__ xs, double* __restrict__ out_f) {
   constexpr int ns = kCell ? 4 : 3;
-  __shared__ double s_yh[kWaves][kWave];
-  __shared__ double s_yl[kWaves][kWave];
   const int lane = threadIdx.x & (kWave - 1);
-  const int wv = threadIdx.x / kWave;
   const int st = lane & 3;
   const uint32_t n_big = ctl->n_big;
   const uint32_t n_groups = (n_big + kWfGroup - 1) / kWfGroup;
@@ -212,49 +223,61 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
       const int64_t o = __shfl_xor(kmax, off);
       kmax = o > kmax ? o : kmax;
     }
-    const double* X = xs + (int64_t)st * n + s;  // (a lane without a chain reads xs[st n], never used)
-    const int64_t lastx = len > 0 ? len - 1 : 0;
+    // a lane without a chain steps along over records 0 .. kmax - 1 (in bounds: kmax <= n), its
+    // result unused
+    const double* X = xs + 4 * s + st;
+    const int64_t clen = mine ? len : kmax;
+    const int64_t lastx = clen > 0 ? clen - 1 : 0;
     double mean = 0.0, m2 = 0.0;
     double xb[kWfBatch], xn[kWfBatch];
 #pragma unroll
-    for (int q = 0; q < kWfBatch; q++) xb[q] = X[q < lastx ? q : lastx];
+    for (int q = 0; q < kWfBatch; q++) xb[q] = X[4 * (q < lastx ? q : lastx)];
     for (int64_t c0 = 0; c0 < kmax; c0 += kWave) {
-      {  // 1 / k for this chunk's 64 record indices, as y_hi + y_lo
-        const double k = (double)(c0 + lane + 1);
-        const double yh = 1.0 / k;
-        s_yh[wv][lane] = yh;
-        s_yl[wv][lane] = __fma_rn(-k, yh, 1.0) * yh;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int64_t c1 = c0 + kWave < kmax ? c0 + kWave : kmax;
-      for (int64_t c = c0; c < c1; c += kWfBatch) {
+      // 1 / k for this chunk's 64 record indices, as y_hi + y_lo, lane i holding k = c0 + i + 1;
+      // the chain reads record q's pair with readlane (a compile-time lane: no LDS latency on it)
+      const double kd = (double)(c0 + lane + 1);
+      const double yh = 1.0 / kd;
+      const double yl = __fma_rn(-kd, yh, 1.0) * yh;
 #pragma unroll
-        for (int q = 0; q < kWfBatch; q++) {
-          const int64_t kq = c + kWfBatch + q;
-          xn[q] = X[kq < lastx ? kq : lastx];
+      for (int hb = 0; hb < kWave / kWfBatch; hb++) {
+        const int64_t c = c0 + hb * kWfBatch;
+        if (c >= kmax) break;  // wave-uniform
+        {  // the next batch's samples: records nb .. nb + kWfBatch - 1
+          const int64_t nb = c + kWfBatch;
+          const bool part = nb < clen && nb + kWfBatch > clen;  // this lane's chain ends inside it
+          if (__builtin_amdgcn_ballot_w64(part) == 0) {  // wave-uniform: one base per lane, no clamps
+            const double* B = nb + kWfBatch <= clen ? X + 4 * nb : xs;  // past its end: unused values
+#pragma unroll
+            for (int q = 0; q < kWfBatch; q++) xn[q] = B[4 * q];
+          } else {
+#pragma unroll
+            for (int q = 0; q < kWfBatch; q++) {
+              const int64_t kq = nb + q;
+              xn[q] = X[4 * (kq < lastx ? kq : lastx)];
+            }
+          }
         }
-        const auto update = [&](int q) {
+        const auto update = [&](int q, bool act) {
           const double delta = xb[q] - mean;
-          mean = mean + __fma_rn(delta, s_yh[wv][c - c0 + q], delta * s_yl[wv][c - c0 + q]);  // + RN(delta / k)
-          const double delta2 = xb[q] - mean;
-          m2 = m2 + delta * delta2;
+          const double h = readlane_f64(yh, hb * kWfBatch + q), l = readlane_f64(yl, hb * kWfBatch + q);
+          const double nm = mean + __fma_rn(delta, h, delta * l);  // + RN(delta / k)
+          const double delta2 = xb[q] - nm;
+          const double nm2 = m2 + delta * delta2;
+          mean = act ? nm : mean;
+          m2 = act ? nm2 : m2;
         };
-        if (c + kWfBatch <= len) {
+        // no lane-divergent branch around the updates: readlane must see y of every lane (a
+        // value computed under a partial exec mask would be stale in the inactive lanes)
+        if (__builtin_amdgcn_ballot_w64(c + kWfBatch > clen) == 0) {  // wave-uniform
 #pragma unroll
-          for (int q = 0; q < kWfBatch; q++) update(q);
+          for (int q = 0; q < kWfBatch; q++) update(q, true);
         } else {
 #pragma unroll
-          for (int q = 0; q < kWfBatch; q++)
-            if (c + q < len) update(q);
+          for (int q = 0; q < kWfBatch; q++) update(q, c + q < clen);
         }
 #pragma unroll
         for (int q = 0; q < kWfBatch; q++) xb[q] = xn[q];
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();  // s_y is rewritten by the next chunk
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     if (mine) {
       double* F = out_f + e * SCT_NF;

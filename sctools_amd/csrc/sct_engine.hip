@@ -113,7 +113,7 @@ Layout layout_for(const sct_plan_t* plan) {
   const bool welford = plan->float_mode == SCT_FLOAT_WELFORD;
   L.wctl = take(welford ? sizeof(WelfordCtl) : 0);
   L.worder = take(welford ? sizeof(uint32_t) * (size_t)L.max_ent : 0);
-  L.wx = take(welford ? sizeof(double) * 4 * (size_t)n1 : 0);  // every record's stream values
+  L.wx = take(welford ? sizeof(double) * 4 * (size_t)(n1 + kWfPad) : 0);  // every record's stream values
   L.total = off;
   return L;
 }

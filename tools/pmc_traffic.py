@@ -44,7 +44,7 @@ def load(path):
     return {k: sum(v) / len(v) for k, v in per.items()}, (torch_last[1] if torch_last else None)
 
 
-def main(d):
+def main(d, extra=()):
     fetch, cf = load(os.path.join(d, "fetch_counter_collection.csv"))
     write, cw = load(os.path.join(d, "write_counter_collection.csv"))
     kernels = {}
@@ -54,7 +54,11 @@ def main(d):
         kernels[k] = {"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w, "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024}
     out = {
         "source_sha256": source_hash(),
-        "workload": "tools/pmc_probe.py: config-2 shard (100M records, 10k cells, 30k genes), cell + grouped gene",
+        "workload": "tools/pmc_probe.py %s: %s, cell + grouped gene" % (" ".join(extra) or "--config 2", {
+            "2": "config-2 shard (100M records, 10k cells, 30k genes)",
+            "4": "config-4 shard (125M records, 62.5k lognormal(0, 2) cells, 30k genes)",
+            "5": "config-5 shard (100M shuffled records sorted by (CB, UB, GE, query name) in the step)"}[
+                extra[extra.index("--config") + 1] if "--config" in extra else "2"]),
         "calibration_1GiB_clone": {"FETCH_SIZE_KiB": cf, "WRITE_SIZE_KiB": cw,
                                    "expected_KiB": 1 << 20, "fetch_correction": 2},
         "kernels": kernels,
@@ -63,4 +67,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2:])
