@@ -7,8 +7,9 @@
 // lane, the overlapping case as src = pos - dist + i mod dist), refilling the compressed-input
 // ring and flushing the window to HBM.
 //
-// LDS per wave (40 KB, four waves per CU): the 32 KB window (a ring: bytes older than 32 KB are
-// already flushed), a 1024-entry literal/length table (10-bit root), a 256-entry distance
+// LDS per wave (~11 KB at the default 4 KB window, 14 waves per CU): the window (a ring of the
+// newest output bytes; older ones are flushed to HBM and read back from there by far matches), a
+// 1024-entry literal/length table (10-bit root), a 256-entry distance
 // table (8-bit root), the canonical code data for codes longer than the root (decoded by the
 // counting method of zlib's puff.c), and a 1 KB ring of compressed words refilled 512 bytes at
 // a time from registers loaded one refill ahead (so the ring never waits on HBM).
@@ -26,7 +27,16 @@
 namespace gb {
 
 constexpr uint32_t kLitBits = 10, kDistBits = 8, kClBits = 7;
-constexpr uint32_t kWin = 32768, kWinMask = kWin - 1, kFlush = 16384;
+// The LDS window holds the newest kWin output bytes; older ones are read back from the member's
+// output in HBM, already flushed there (pos - flushed <= kFlush + 258 < kWin at every copy), so a
+// smaller window costs only those far matches and buys waves per CU (24M-record BAM: inflate
+// 0.459 s with a 32 KB window at 4 waves per CU, 0.347 s at 16 KB, 0.246 s at 8 KB, 0.180 s at 4 KB).
+#ifndef SCT_INFL_WIN
+#define SCT_INFL_WIN 4096
+#endif
+constexpr uint32_t kWin = SCT_INFL_WIN, kWinMask = kWin - 1, kFlush = kWin / 4;
+static_assert((kWin & (kWin - 1)) == 0 && kWin >= 2048 && kWin <= 32768, "a power-of-two window");
+static_assert(kFlush + 2 * 258 < kWin, "unflushed bytes always sit in the window, clear of a far copy");
 constexpr uint32_t kRingW = 256, kRingMask = kRingW - 1, kRingHalf = 128;
 
 // table entry: bits 0..3 code length, 4..6 kind, 8..12 extra bits, 16..31 value
@@ -223,6 +233,10 @@ __device__ __forceinline__ void flush_to(InflateLds& S, uint8_t* out, uint32_t& 
                                          uint32_t lane) {
   for (uint32_t j = flushed + lane; j < upto; j += 64) out[j] = S.win[j & kWinMask];
   flushed = upto;
+  // far matches read flushed bytes back from HBM, other lanes' stores: a workgroup-scope
+  // release / acquire pair (the wave is the workgroup) makes them visible to every lane
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // One wave per member.  status[m]: ST_* (0 = the member's payload is in out[out_off, +isize)).
@@ -263,7 +277,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in, 
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(src) + q;
       for (uint32_t done = 0; done < len;) {
         if (pos - flushed >= kFlush) flush_to(S, out, flushed, flushed + kFlush, lane);
-        const uint32_t c = min(len - done, 4096u);
+        const uint32_t c = min(len - done, kFlush);
         for (uint32_t j = lane; j < c; j += 64) S.win[(pos + j) & kWinMask] = sb[done + j];
         pos += c;
         done += c;
@@ -374,14 +388,24 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t* __restrict__ in, 
       drop(b, dx);
       if (dist > pos) { st = ST_DIST; break; }
       if (pos + len > isize) { st = ST_SIZE; break; }
-      for (uint32_t j = lane; j < len; j += 64) {
-        uint32_t r = j;
-        if (dist < len) {  // overlapping: the last `dist` bytes repeat
-          r = j - (uint32_t)((float)j * __frcp_rn((float)dist)) * dist;
-          r = (int)r < 0 ? r + dist : r;
-          r = r >= dist ? r - dist : r;
+      if (dist <= kWin) {  // wave-uniform: every source byte is in the window
+        for (uint32_t j = lane; j < len; j += 64) {
+          uint32_t r = j;
+          if (dist < len) {  // overlapping: the last `dist` bytes repeat
+            r = j - (uint32_t)((float)j * __frcp_rn((float)dist)) * dist;
+            r = (int)r < 0 ? r + dist : r;
+            r = r >= dist ? r - dist : r;
+          }
+          S.win[(pos + j) & kWinMask] = S.win[(pos - dist + r) & kWinMask];
         }
-        S.win[(pos + j) & kWinMask] = S.win[(pos - dist + r) & kWinMask];
+      } else {  // a far match (len <= 258 < dist): its older bytes come from the flushed output
+        // a source byte is read from the window only if no destination of this copy shares its
+        // slot (p >= pos + len - kWin: an earlier 64-byte round could have overwritten it); the
+        // others were flushed (flushed > pos - kFlush - 258 > pos + len - kWin)
+        for (uint32_t j = lane; j < len; j += 64) {
+          const uint32_t p = pos - dist + j;
+          S.win[(pos + j) & kWinMask] = dist - j + len <= kWin ? S.win[p & kWinMask] : out[p];
+        }
       }
       pos += len;
     }

@@ -20,7 +20,7 @@ from typing import Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsct_gbam.so")
+LIB_PATH = os.environ.get("SCT_GBAM_LIB_PATH") or os.path.join(HERE, "libsct_gbam.so")  # override: experiments only
 
 OK, HOST = 0, 1
 _MODES = {"cell": 0, "gene": 1}
