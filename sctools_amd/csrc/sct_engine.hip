@@ -353,6 +353,56 @@ int launch_build_keys(bool cell, bool gene, dim3 grid, hipStream_t s, const KeyC
   return SCT_OK;
 }
 
+// Sequential Welford (SCT_FLOAT_WELFORD): big entities one wave each (largest first), small ones a
+// lane each.  It needs only the entity starts, the input columns and its own workspace, and writes
+// only the mean / variance slots of the output rows (k_finalize writes the others), so it runs on a
+// side stream from the moment the entity starts exist, beside the key pass' successors (bucket
+// partition, hash tiles) on the caller's stream.
+struct WelfordSide {
+  hipStream_t s2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  ~WelfordSide() {  // the caller's stream waits on `join` before anything after the pipeline runs
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+    if (s2) (void)hipStreamDestroy(s2);
+  }
+};
+
+int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent, const RecCols& rc2,
+                  const int64_t* ent_start, double* out_f, hipStream_t s, WelfordSide& wf) {
+  HIPCHK(hipStreamCreateWithFlags(&wf.s2, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&wf.fork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&wf.join, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(wf.fork, s));
+  HIPCHK(hipStreamWaitEvent(wf.s2, wf.fork, 0));
+  hipStream_t s2 = wf.s2;
+  const dim3 egrid((unsigned)cdiv(n_ent, kBlock));
+  if (n >= kWfWave) {
+    WelfordCtl* wc = at<WelfordCtl>(ws, L.wctl);
+    uint32_t* worder = at<uint32_t>(ws, L.worder);
+    HIPCHK(hipMemsetAsync(wc, 0, sizeof(WelfordCtl), s2));
+    LAUNCH("welford_bins", k_welford_bins, egrid, dim3(kBlock), s2, ent_start, n_ent, n, wc);
+    LAUNCH("welford_order", k_welford_order, egrid, dim3(kBlock), s2, ent_start, n_ent, n, wc, worder);
+    double* xs = at<double>(ws, L.wx);
+    const dim3 xgrid((unsigned)cdiv(n, kBlock));
+    if (cell) {
+      LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s2, rc2, n, xs);
+      LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s2, ent_start, n_ent, n,
+               (const uint32_t*)worder, wc, (const double*)xs, out_f);
+    } else {
+      LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s2, rc2, n, xs);
+      LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfBlocks), dim3(kBlock), s2, ent_start, n_ent, n,
+               (const uint32_t*)worder, wc, (const double*)xs, out_f);
+    }
+  }
+  if (cell) {
+    LAUNCH("welford", k_welford<true>, egrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n, out_f);
+  } else {
+    LAUNCH("welford", k_welford<false>, egrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n, out_f);
+  }
+  return SCT_OK;
+}
+
 int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* gene_is_mito, void* ws,
              size_t ws_bytes, int64_t* out_i, double* out_f, int64_t capacity, int64_t* n_rows,
              int64_t* gene_partials, hipStream_t s, bool allow_bucket = true) {
@@ -466,14 +516,21 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     if (err & 2) return fail(SCT_EINVAL, "a gene / cell / umi id lies outside its dictionary size");
   }
   if (rc) return rc;
+  WelfordSide wf;
+  if (!exact && out_i) {  // the entity starts exist now (k_level1_plan or the key pass)
+    rc = welford_stage(L, ws, cell, n, n_ent, rc2, ent_start, out_f, s, wf);
+    if (rc) return rc;
+  }
 
   // 2-3. distinct counts (+ per-record distinct events for the gene view)
   uint16_t* dflags = gene ? at<uint16_t>(ws, L.dflags) : nullptr;
   if (bucket) {
     rc = bucket_distinct(L, ws, n, n_ent, ent_start, mito, b, cell, gene, partials, dflags, planned, s);
-    if (rc == 1)  // a mapped ref id does not fit the bucket payload: redo on the global-sort path
+    if (rc == 1) {  // a mapped ref id does not fit the bucket payload: redo on the global-sort path
+      if (wf.s2) HIPCHK(hipStreamSynchronize(wf.s2));  // (its workspace is reused by the redo)
       return pipeline(plan, rec, gene_is_mito, ws, ws_bytes, out_i, out_f, capacity, n_rows, gene_partials, s,
                       false);
+    }
     if (rc) return rc;
   } else {
     int which = 0;
@@ -497,32 +554,9 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   if (out_i) {
     LAUNCH("finalize", k_finalize, dim3((unsigned)cdiv(n_ent * kFinThreads, kBlock)), dim3(kBlock), s, (const int64_t*)partials,
            n_ent, cell ? SCT_MODE_CELL : SCT_MODE_GENE, exact ? 1 : 0, (const int64_t*)ent_start, out_i, out_f);
-    if (!exact) {  // sequential Welford: big entities one wave each (largest first), small ones a lane each
-      const dim3 egrid((unsigned)cdiv(n_ent, kBlock));
-      if (n >= kWfWave) {
-        WelfordCtl* wc = at<WelfordCtl>(ws, L.wctl);
-        uint32_t* worder = at<uint32_t>(ws, L.worder);
-        HIPCHK(hipMemsetAsync(wc, 0, sizeof(WelfordCtl), s));
-        LAUNCH("welford_bins", k_welford_bins, egrid, dim3(kBlock), s, (const int64_t*)ent_start, n_ent, n, wc);
-        LAUNCH("welford_order", k_welford_order, egrid, dim3(kBlock), s, (const int64_t*)ent_start, n_ent, n, wc,
-               worder);
-        double* xs = at<double>(ws, L.wx);
-        const dim3 xgrid((unsigned)cdiv(n, kBlock));
-        if (cell) {
-          LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s, rc2, n, xs);
-          LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s,
-                   (const int64_t*)ent_start, n_ent, n, (const uint32_t*)worder, wc, (const double*)xs, out_f);
-        } else {
-          LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s, rc2, n, xs);
-          LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfBlocks), dim3(kBlock), s,
-                   (const int64_t*)ent_start, n_ent, n, (const uint32_t*)worder, wc, (const double*)xs, out_f);
-        }
-      }
-      if (cell) {
-        LAUNCH("welford", k_welford<true>, egrid, dim3(kBlock), s, rc2, (const int64_t*)ent_start, n_ent, n, out_f);
-      } else {
-        LAUNCH("welford", k_welford<false>, egrid, dim3(kBlock), s, rc2, (const int64_t*)ent_start, n_ent, n, out_f);
-      }
+    if (!exact) {  // launched on the side stream after the key pass (welford_stage): joined here
+      HIPCHK(hipEventRecord(wf.join, wf.s2));
+      HIPCHK(hipStreamWaitEvent(s, wf.join, 0));
     }
   }
   if (gene) {

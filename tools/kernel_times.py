@@ -38,9 +38,16 @@ def main():
     if a.only:
         variants = {k: v for k, v in variants.items() if k in a.only.split(",")}
     out = {}
+    import time
+
     for name, fn in variants.items():
         fn()
         torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            fn()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / a.reps * 1e3
         eng.profile_enable(True)
         for _ in range(a.reps):
             fn()
@@ -49,6 +56,7 @@ def main():
         prof = eng.profile_read()
         out[name] = {k: round(v[0] / a.reps, 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1][0])}
         out[name]["_total"] = round(sum(v[0] for v in prof.values()) / a.reps, 4)
+        out[name]["_wall_ms"] = round(wall, 4)  # the call's wall time, kernels unprofiled (side streams overlap)
     print(json.dumps(out, indent=1))
 
 
