@@ -15,7 +15,10 @@ namespace sct {
 constexpr int kItems = 16;
 constexpr int kTile = kBlock * kItems;  // 4096 records per tile (entity-run heads, key pass)
 // LSD radix sort tiles: 2048 items (24 KB of keys / values staged in LDS, so 6 blocks fit a CU)
-constexpr int kSortItems = 8;
+#ifndef SCT_SORT_ITEMS
+#define SCT_SORT_ITEMS 8
+#endif
+constexpr int kSortItems = SCT_SORT_ITEMS;
 constexpr int kSortTile = kBlock * kSortItems;
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
