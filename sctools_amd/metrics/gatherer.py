@@ -12,8 +12,8 @@ The per-record aggregation runs on the GPU (``sctools_amd.engine``): a BAM is
 inflated and parsed into columns on the same GPU (``sctools_amd.gbam``; a file
 it declines -- one the reference rejects -- is decoded on the host by
 ``sctools_amd.columnar``, raising the same exception types the reference
-raises), and the HIP engine computes every row in one launch sequence.  ``float_mode='welford'`` (default) reproduces the
-reference's sequential Welford floats bit for bit; ``'exact'`` computes
+raises), and the HIP engine computes every row in one launch sequence.
+``float_mode='welford'`` (default) reproduces the reference's sequential Welford floats bit for bit; ``'exact'`` computes
 correctly rounded mean / variance from exact sums (order independent,
 within 1e-12 of Welford).
 
@@ -83,18 +83,23 @@ class MetricGatherer:
         self._float_mode = float_mode
         self._device = device
         self._devices = devices  # None: one device (`device`); int N or device list: multigpu
-        self._gpu_decode = gpu_decode  # one device: inflate and parse a BAM on it (gbam)
+        self._gpu_decode = gpu_decode  # inflate and parse a BAM on the (first) device (gbam)
 
     def _columns(self, mode: str, metric_mode: str) -> columnar.Columns:
-        """The file's columns: decoded on the GPU that computes the metrics when there is one
-        device and the input is BAM (a file the device decoder declines goes through the host
-        decoder, which raises the reference's exception), else on the host."""
-        if self._devices is None and self._gpu_decode and mode == "rb":
+        """The file's columns: a BAM is decoded on the GPU that computes the metrics (the first of
+        several devices); a file the device decoder declines, and SAM text, go through the host
+        decoder, which raises the reference's exception."""
+        if self._gpu_decode and mode == "rb":
             from sctools_amd import engine as E
             from sctools_amd import gbam
 
             if gbam.available():
-                dev = E.get_engine(self._device).device
+                if self._devices is None:
+                    dev = E.get_engine(self._device).device
+                else:  # several devices: decode on the first, the shards are copied device to device
+                    from sctools_amd import multigpu
+
+                    dev = E.get_engine(multigpu.parse_devices(self._devices)[0]).device
                 return columnar.columnarize(self.bam_file, mode, metric_mode, device=dev)
         return columnar.columnarize(self.bam_file, mode, metric_mode)
 
@@ -159,7 +164,7 @@ class GatherCellAndGeneMetrics(MetricGatherer):
     def extract_metrics(self, mode: str = "rb") -> None:
         from sctools_amd import multigpu
 
-        cols = columnar.columnarize(self.bam_file, mode, columnar.MODE_CELL)
+        cols = self._columns(mode, columnar.MODE_CELL)
         (ci, cf), (gi, gf) = multigpu.compute_cell_and_gene_rows(cols, self._mitochondrial_gene_ids,
                                                                  self._float_mode, self._devices)
         with MetricCSVWriter(self._output_stem, self._compress) as out:

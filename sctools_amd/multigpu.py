@@ -248,8 +248,15 @@ class DeviceGroup:
         self.close()
 
 
-def _shard_arrays(arrays, lo, hi):
-    return {c: np.ascontiguousarray(a[lo:hi]) for c, a in arrays.items()}
+def _shard_to(cols: columnar.Columns, lo: int, hi: int, device) -> dict:
+    """Records [lo, hi) of every column on ``device``: host columns are copied up; device columns
+    (decoded on the GPU, ``gbam``) are sliced in place and copied device to device (over xGMI when
+    the shard's device is another GPU)."""
+    from sctools_amd import engine as E
+
+    if not cols.on_device:
+        return E.to_device({c: np.ascontiguousarray(a[lo:hi]) for c, a in cols.arrays.items()}, device)
+    return {c: t[lo:hi].to(device, copy=True) for c, t in cols.arrays.items()}  # (fresh, aligned buffers)
 
 
 def _dims(cols: columnar.Columns):
@@ -275,7 +282,7 @@ def compute_rows(cols: columnar.Columns, mode: str, mitochondrial_gene_ids=froze
             if hi == lo:
                 return np.zeros((0, N.SCT_NI), np.int64), np.zeros((0, N.SCT_NF), np.float64)
             eng = g.engines[r]
-            dev_cols = E.to_device(_shard_arrays(cols.arrays, lo, hi), eng.device)
+            dev_cols = _shard_to(cols, lo, hi, eng.device)
             gm = torch.from_numpy(mito).to(eng.device)
             gx = torch.from_numpy(multi).to(eng.device)
             ints, floats = eng.compute(dev_cols, mode, dims, gm, gx, float_mode=float_mode)
@@ -297,8 +304,14 @@ def compute_cell_and_gene_rows(cols: columnar.Columns, mitochondrial_gene_ids=fr
 
     cell = cols.arrays["cell"]
     if cell.shape[0]:  # grouped gene rows need every cell in ONE run (the cell-sharding invariant)
-        heads = cell[np.concatenate(([0], np.flatnonzero(cell[1:] != cell[:-1]) + 1))]
-        if np.bincount(heads).max() > 1:
+        if cols.on_device:
+            heads = cell[torch.cat((torch.zeros(1, dtype=torch.long, device=cell.device),
+                                    torch.nonzero(cell[1:] != cell[:-1]).flatten() + 1))]
+            twice = int(torch.bincount(heads.long()).max().item()) > 1
+        else:
+            heads = cell[np.concatenate(([0], np.flatnonzero(cell[1:] != cell[:-1]) + 1))]
+            twice = np.bincount(heads).max() > 1
+        if twice:
             raise ValueError("gene rows of a record set need cell-sorted records (a cell barcode forms two runs)")
     mito, multi = cols.gene_flags(mitochondrial_gene_ids)
     dims = _dims(cols)
@@ -309,7 +322,7 @@ def compute_cell_and_gene_rows(cols: columnar.Columns, mitochondrial_gene_ids=fr
         def rank_rows(r):
             lo, hi = bounds[r]
             eng = g.engines[r]
-            dev_cols = E.to_device(_shard_arrays(cols.arrays, lo, hi), eng.device)
+            dev_cols = _shard_to(cols, lo, hi, eng.device)
             gm = torch.from_numpy(mito).to(eng.device)
             gx = torch.from_numpy(multi).to(eng.device)
             if hi == lo:
