@@ -54,7 +54,8 @@ int sct_gbam_dictionary(const sct_gbam_t* h, int32_t which, int64_t* n, const ch
  * (tests compare it with zlib).  *total (if set) receives the payload length. */
 int sct_gbam_read_inflated(const sct_gbam_t* h, uint64_t off, uint64_t n, void* dst, uint64_t* total);
 
-/* Seconds spent per stage: [0] map + scan, [1] copy to the device, [2] inflate, [3] record
+/* Seconds spent per stage: [0] map + scan, [1] copy to the device (in pieces, each piece's members
+ * inflating while the next piece copies), [2] the inflate left after the last piece, [3] record
  * starts, [4] parse + intern, [5] dictionaries, [6] members, [7] record-start repair rounds. */
 int sct_gbam_timing(const sct_gbam_t* h, double* t8);
 
