@@ -122,11 +122,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    # rehearsal of the N-rank path on a one-GPU box (tests only, never a scaling number): every rank
+    # on cuda:0, the collectives over gloo (RCCL holds one rank per device)
+    share = os.environ.get("SCT_BENCH_SHARE_DEVICE") == "1"
+    if share:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from sctools_amd import distributed as D
     from sctools_amd import engine as E
@@ -308,7 +316,7 @@ def main():
                 "genes": args.genes,
                 "float_mode": args.float_mode,
                 "umi_bits": args.umi_bits,
-                "parallelism": "cell-sharded x%d" % world,
+                "parallelism": "cell-sharded x%d" % world + (" (rehearsal: ranks share cuda:0, gloo)" if share else ""),
             },
             "roofline": roofline,
             "kernel_ms_per_step": kernel_ms_per_step,
