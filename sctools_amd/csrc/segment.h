@@ -648,7 +648,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
       int64_t e = cur_e;
       if (!one_run) {
         e = valid ? ebase + (int64_t)loc_of(q, s_hb, s_wpre) : cur_e;
-        wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
+#ifndef SCT_PACKED_FLUSH
+#define SCT_PACKED_FLUSH 1
+#endif
+        if (SCT_PACKED_FLUSH)  // per-lane counts <= kKItems between flushes: 16-bit fields suffice
+          wave_flush_packed16<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
+        else
+          wave_flush<A::kK>(acc.v, valid && e != cur_e && cur_e >= 0, cur_e, partials, slot);
         if (!valid) continue;
         cur_e = e;
       }
@@ -718,7 +724,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
       }
     }
   }
-  wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
+  if (SCT_PACKED_FLUSH)
+    wave_flush_packed16<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
+  else
+    wave_flush<A::kK>(acc.v, cur_e >= 0, cur_e, partials, slot);
   if (kGene) {
     __syncthreads();
     // the tile's range in each present bucket: its offset inside the bucket (k_gene_emit)

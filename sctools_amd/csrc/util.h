@@ -420,4 +420,38 @@ __device__ __forceinline__ void wave_flush(T (&v)[K], bool member, int64_t e, in
   }
 }
 
+
+// wave_flush for small non-negative int32 counters (every lane's v[i] < 2^10, so a field's wave sum
+// stays below 2^16): two counters per 32-bit word, one DPP reduction per word -- half the
+// reductions of wave_flush (the key pass's 13 record counters, flushed at every run boundary).
+template <int K, typename SlotOf>
+__device__ __forceinline__ void wave_flush_packed16(int32_t (&v)[K], bool member, int64_t e,
+                                                    int64_t* __restrict__ rows, SlotOf slot_of) {
+  static_assert(K <= kWave, "one lane per slot");
+  constexpr int W = (K + 1) / 2;
+  const int lane = threadIdx.x & (kWave - 1);
+  uint64_t pending = __ballot(member);
+  while (pending) {
+    const int lead = __ffsll((unsigned long long)pending) - 1;
+    const int64_t el = __shfl(e, lead);
+    const bool in = member && e == el;
+    int32_t tot[W];
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const uint32_t lo = in ? (uint32_t)v[2 * w] : 0u;
+      const uint32_t hi = (in && 2 * w + 1 < K) ? (uint32_t)v[2 * w + 1] : 0u;
+      tot[w] = wave_sum_dpp((int32_t)(lo | (hi << 16)));
+    }
+    int64_t mine = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++) mine = (lane == i) ? (int64_t)(((uint32_t)tot[i / 2] >> (16 * (i % 2))) & 0xffffu) : mine;
+    if (lane < K && mine) atomicAdd((unsigned long long*)&rows[el * SCT_NP + slot_of(lane)], (unsigned long long)mine);
+    if (in) {
+#pragma unroll
+      for (int i = 0; i < K; i++) v[i] = 0;
+    }
+    pending &= ~__ballot(in);
+  }
+}
+
 }  // namespace sct
