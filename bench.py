@@ -68,7 +68,22 @@ ALG_BYTES = {
 
 
 # HIP-event kernel names (engine profile) -> rocprofv3 kernel names (tools/pmc_traffic.py keys)
-PMC_NAMES = {"build_keys": "build_keys_run", "scan": "scan_wide", "heads": "heads4"}
+# engine profile names -> the kernels (rocprofv3 names, sct::k_*) launched under them; a name
+# covering several kernels gets their dispatch-weighted mean bytes per launch
+PMC_NAMES = {"build_keys": ["build_keys_run"], "heads": ["heads4", "heads"],
+             "scan": ["scan_wide", "scan_reduce", "scan_small", "scan_apply"],
+             "tag_pack": ["pack"], "tag_keys": ["field_keys", "round_keys"], "tag_ties": ["tie_wave"],
+             "tag_long_keys": ["long_keys"], "tag_long_scatter": ["long_scatter"], "tag_unpack": ["unpack"],
+             "tag_row_hist": ["row_hist"], "tag_row_scatter": ["row_scatter"]}
+
+
+def pmc_bytes_per_launch(d, name):
+    """HBM bytes per launch of profile name `name` from a pmc_traffic.json, or None."""
+    ks = [k for k in PMC_NAMES.get(name, [name]) if k in d.get("kernels", {})]
+    if not ks:
+        return None
+    w = [max(1, d["kernels"][k].get("dispatches", 1)) for k in ks]
+    return sum(d["kernels"][k]["hbm_bytes_per_launch"] * x for k, x in zip(ks, w)) / sum(w)
 
 
 def pipeline_bytes(args, dims):
@@ -405,10 +420,16 @@ def _traffic_file(args):
     from pmc_traffic import source_hash
 
     path = args.traffic_json
-    if not path or not os.path.exists(path) or args.records != 100_000_000 or args.cells != 10_000:
+    if not path or not os.path.exists(path):
         return None
     d = json.load(open(path))
     if d.get("source_sha256") != source_hash(ROOT):
+        return None
+    # the probe's workload must be this run's: tools/pmc_probe.py --config N at the config's sizes
+    w = d.get("workload", "")
+    cfg = int(w.split("--config ")[1].split()[0].rstrip(":")) if "--config " in w else 2
+    sizes = {2: (100_000_000, 10_000), 4: (125_000_000, 62_500), 5: (100_000_000, 10_000)}[cfg]
+    if cfg != args.config or (args.records, args.cells) != sizes:
         return None
     return d
 
@@ -422,10 +443,10 @@ def pmc_step_traffic(args, table):
         return None
     tot = 0.0
     for k, v in table.items():
-        pk = PMC_NAMES.get(k, k)
-        if pk not in d["kernels"]:
+        b = pmc_bytes_per_launch(d, k)
+        if b is None:
             return None
-        tot += d["kernels"][pk]["hbm_bytes_per_launch"] * v[1] / PROFILE_STEPS
+        tot += b * v[1] / PROFILE_STEPS
     return tot
 
 
@@ -434,10 +455,10 @@ def pmc_traffic(args, kernel):
     (tools/pmc_passes.sh -> tools/pmc_traffic.py), if it was measured on this engine source and
     this workload; else None (the roofline then reports traffic null)."""
     d = _traffic_file(args)
-    kernel = PMC_NAMES.get(kernel, kernel)
-    if d is None or kernel not in d.get("kernels", {}):
+    b = pmc_bytes_per_launch(d, kernel) if d is not None else None
+    if b is None:
         return None
-    return d["kernels"][kernel]["hbm_bytes_per_launch"], os.path.relpath(args.traffic_json, ROOT)
+    return b, os.path.relpath(args.traffic_json, ROOT)
 
 
 def cpu_baseline(data, args):

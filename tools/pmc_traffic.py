@@ -41,7 +41,7 @@ def load(path):
             did = int(r["Dispatch_Id"])
             if torch_last is None or did > torch_last[0]:
                 torch_last = (did, v)
-    return {k: sum(v) / len(v) for k, v in per.items()}, (torch_last[1] if torch_last else None)
+    return {k: (sum(v) / len(v), len(v)) for k, v in per.items()}, (torch_last[1] if torch_last else None)
 
 
 def main(d, extra=()):
@@ -49,9 +49,10 @@ def main(d, extra=()):
     write, cw = load(os.path.join(d, "write_counter_collection.csv"))
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
-        f = fetch.get(k, 0.0)
-        w = write.get(k, 0.0)
-        kernels[k] = {"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w, "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024}
+        f, nf = fetch.get(k, (0.0, 0))
+        w, nw = write.get(k, (0.0, 0))
+        kernels[k] = {"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w, "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
+                      "dispatches": max(nf, nw)}  # in the probe run: weights kernels sharing a profile name
     out = {
         "source_sha256": source_hash(),
         "workload": "tools/pmc_probe.py %s: %s, cell + grouped gene" % (" ".join(extra) or "--config 2", {
