@@ -41,6 +41,7 @@ namespace gb {
 
 constexpr uint64_t kUnknown = ~0ull, kBadWalk = ~0ull - 1;
 constexpr uint32_t kScan = 1u << 18;  // bytes a member's start guess looks through
+constexpr int kStartRounds = 512;      // record-start repair rounds before the file goes to the host decoder
 constexpr uint64_t kPad = 1u << 16;   // readable bytes after the file image and after U
 
 __device__ __forceinline__ uint32_t u16(const uint8_t* U, uint64_t p) { return U[p] | (uint32_t)U[p + 1] << 8; }
@@ -131,15 +132,27 @@ __global__ void k_walk(const uint8_t* __restrict__ U, uint64_t ulen, const uint6
   land[m + 1] = p;
 }
 
-// Replace every start that disagrees with its predecessor's landing; count the disagreements
-// (S[n_mem] = ulen is fixed: a landing elsewhere stays a disagreement).
+// ag[m]: member m's start agrees with its predecessor's landing this round (mH: exact by
+// construction).  Computed before k_fix rewrites any start.
+__global__ void k_agree(uint32_t mH, uint32_t n_mem, const uint64_t* __restrict__ S,
+                        const uint64_t* __restrict__ land, uint8_t* __restrict__ ag) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m > n_mem) return;
+  ag[m] = m < mH ? 0 : (m == mH || land[m] == S[m]) ? 1 : 0;
+}
+
+// Replace a start that disagrees with its predecessor's landing -- only when the predecessor's own
+// start agreed (a landing walked from a wrong start would carry the error forward one member per
+// round); count the disagreements (S[n_mem] = ulen is fixed: a landing elsewhere stays one).
+// Each round the agreeing prefix from mH grows past at least one more member, and a run of k
+// wrong guesses takes k rounds.
 __global__ void k_fix(uint32_t mH, uint32_t n_mem, uint64_t* __restrict__ S, const uint64_t* __restrict__ land,
-                      uint32_t* __restrict__ n_bad) {
+                      const uint8_t* __restrict__ ag, uint32_t* __restrict__ n_bad) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m <= mH || m > n_mem) return;
   const uint64_t l = land[m];
   if (l == S[m]) return;
-  if (m < n_mem && l != kUnknown && l != kBadWalk) S[m] = l;
+  if (m < n_mem && ag[m - 1] && l != kUnknown && l != kBadWalk) S[m] = l;
   atomicAdd(n_bad, 1u);
 }
 
@@ -726,13 +739,18 @@ int open_impl(const char* path, int32_t device, void* stream, sct_gbam_t** out, 
   HIPOK(d_cnt.alloc(n_mem));
   HIPOK(d_base.alloc(n_mem + 1));
   hipLaunchKernelGGL(k_guess, dim3(grid(n_mem, 64)), dim3(64), 0, st, G->u.p, ulen, d_O.p, mH, n_mem, H, d_S.p);
+  DevBuf<uint8_t> d_ag;
+  HIPOK(d_ag.alloc(n_mem + 1));
   int rounds = 0;
   for (;; rounds++) {
-    if (rounds == 64) return gfail(SCT_GBAM_HOST, "record starts did not converge");
+    if (rounds == kStartRounds) return gfail(SCT_GBAM_HOST, "record starts did not converge");
     hipLaunchKernelGGL(k_walk, dim3(grid(n_mem, 64)), dim3(64), 0, st, G->u.p, ulen, d_O.p, mH, n_mem, d_S.p,
                        d_cnt.p, d_land.p, (uint64_t*)nullptr, (const uint64_t*)nullptr);
     HIPOK(hipMemsetAsync(d_flag.p, 0, sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_fix, dim3(grid(n_mem + 1, 256)), dim3(256), 0, st, mH, n_mem, d_S.p, d_land.p, d_flag.p);
+    hipLaunchKernelGGL(k_agree, dim3(grid(n_mem + 1, 256)), dim3(256), 0, st, mH, n_mem, (const uint64_t*)d_S.p,
+                       (const uint64_t*)d_land.p, d_ag.p);
+    hipLaunchKernelGGL(k_fix, dim3(grid(n_mem + 1, 256)), dim3(256), 0, st, mH, n_mem, d_S.p, d_land.p,
+                       (const uint8_t*)d_ag.p, d_flag.p);
     uint32_t nbad = 0;
     HIPOK(hipMemcpyAsync(&nbad, d_flag.p, sizeof(nbad), hipMemcpyDeviceToHost, st));
     HIPOK(hipStreamSynchronize(st));

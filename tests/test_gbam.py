@@ -161,3 +161,24 @@ def test_corrupt_member_declines(tmp_path):
         assert gbam.decode(path, "cell") is None
         return
     same_as_host(path, "cell")  # the flip left a valid stream: both decoders read the same bytes
+
+
+@pytest.mark.gpu
+def test_repeated_records_converge(tmp_path):
+    """Identical consecutive records (each of small-gene-sorted.bam's records 20 times, 240k records,
+    ~1600 members): a few members' start guesses land inside a record, and the repair must fix each
+    from its agreeing predecessor instead of carrying a wrong landing forward member by member (it
+    used to give up after 64 rounds and hand the file to the host decoder)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import e2e_bench
+
+    path = str(tmp_path / "rep.bam")
+    e2e_bench.make_gene_bam(path, 240_000, 20, procs=4)
+    tm = {}
+    got = gbam.decode(path, "gene", timings=tm)
+    assert got is not None, gbam.last_error()
+    assert tm["start_rounds"] < 64
+    same_as_host(path, "gene")
+    same_as_host(path, "cell")

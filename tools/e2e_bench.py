@@ -25,6 +25,7 @@ from multiprocessing import Pool
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 FIXTURE = os.path.join(ROOT, "tests", "golden", "bam", "small-cell-sorted.bam")
+GENE_FIXTURE = os.path.join(ROOT, "tests", "golden", "bam", "small-gene-sorted.bam")
 EOF_MEMBER = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
 BLOCK = 0xff00
 
@@ -83,6 +84,43 @@ def _group(args):
     return _bgzf(b"".join(parts))
 
 
+def _group_gene(args):
+    """Gene-sorted replicas [lo, hi): the fixture's records each repeated k times (gene runs k times
+    longer), the first 3 characters of every GE value replaced by replica r's code (new genes)."""
+    lo, hi, k = args
+    parts = []
+    for r in range(lo, hi):
+        code = bytes(65 + (r // 26 ** i) % 26 for i in range(3))
+        parts.append(re.sub(rb"GEZ[^\x00]{3}", b"GEZ" + code, _BODY))
+    return _bgzf(b"".join(parts))
+
+
+def make_gene_bam(path, records, per_run, procs=16):
+    """A gene-sorted BAM (small-gene-sorted.bam: 300 records of 8 genes) for GatherGeneMetrics."""
+    raw = _payload(GENE_FIXTURE)
+    h = _header_end(raw)
+    body = raw[h:]
+    recs, off = [], 0
+    while off < len(body):
+        n = 4 + struct.unpack_from("<i", body, off)[0]
+        recs.append(body[off:off + n])
+        off += n
+    body = b"".join(r * per_run for r in recs)
+    n_body = len(recs) * per_run
+    reps = (records + n_body - 1) // n_body
+    if reps > 26 ** 3:
+        raise ValueError("too many replicas for 3-letter gene codes")
+    jobs = [(lo, min(reps, lo + 16), per_run) for lo in range(0, reps, 16)]
+    with open(path + ".tmp", "wb") as f:
+        f.write(_bgzf(raw[:h]))
+        with Pool(procs, initializer=_init, initargs=(body,)) as pool:
+            for blob in pool.imap(_group_gene, jobs):
+                f.write(blob)
+        f.write(EOF_MEMBER)
+    os.replace(path + ".tmp", path)
+    return reps * n_body
+
+
 def make_bam(path, records, per_cell, procs=16):
     raw = _payload(FIXTURE)
     h = _header_end(raw)
@@ -108,7 +146,13 @@ def main():
     ap.add_argument("--bam", default=None)
     ap.add_argument("--host-decoder", action="store_true")
     ap.add_argument("--float-mode", default="welford")
+    ap.add_argument("--gene", action="store_true",
+                    help="GatherGeneMetrics on a gene-sorted BAM (small-gene-sorted.bam, each record "
+                         "repeated --records-per-run times, gene names renamed per replica) instead")
+    ap.add_argument("--records-per-run", type=int, default=20)
     a = ap.parse_args()
+    if a.gene:
+        return main_gene(a)
     bam = a.bam or "/tmp/sct_e2e_%d.bam" % a.records
     if not os.path.exists(bam):
         t0 = time.time()
@@ -169,6 +213,46 @@ def main():
 
         same = gzip.open("/tmp/sct_e2e_cell2.csv.gz").read() == gzip.open("/tmp/sct_e2e_cell3.csv.gz").read()
         res["device_and_host_decoder_csv_identical"] = same
+    print(json.dumps(res))
+
+
+def main_gene(a):
+    bam = a.bam or "/tmp/sct_e2e_gene_%d.bam" % a.records
+    if not os.path.exists(bam):
+        t0 = time.time()
+        n = make_gene_bam(bam, a.records, a.records_per_run)
+        print("wrote %s (%d records, %.0f MB) in %.1fs" % (bam, n, os.path.getsize(bam) / 1e6, time.time() - t0),
+              file=sys.stderr, flush=True)
+    import torch
+
+    from sctools_amd.metrics import gatherer as G
+
+    torch.cuda.init()
+    res = {"bam": bam, "bam_mb": os.path.getsize(bam) / 1e6, "float_mode": a.float_mode, "entry": "GatherGeneMetrics"}
+    with open(bam, "rb") as f:
+        while f.read(1 << 26):
+            pass
+    G.GatherGeneMetrics(bam, "/tmp/sct_e2e_gene_warm", float_mode=a.float_mode).extract_metrics()
+    torch.cuda.synchronize()
+    runs = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        G.GatherGeneMetrics(bam, "/tmp/sct_e2e_gene", float_mode=a.float_mode).extract_metrics()
+        runs.append(time.perf_counter() - t0)
+    from sctools_amd import bamnative
+
+    n = int(bamnative.decode(bam, "gene")[0]["cell"].shape[0]) if a.host_decoder else None
+    res["GatherGeneMetrics_s"] = runs
+    if a.host_decoder:
+        t0 = time.perf_counter()
+        G.GatherGeneMetrics(bam, "/tmp/sct_e2e_gene_host", float_mode=a.float_mode, gpu_decode=False).extract_metrics()
+        res["GatherGeneMetrics_host_decoder_s"] = time.perf_counter() - t0
+        import gzip
+
+        res["device_and_host_decoder_csv_identical"] = (gzip.open("/tmp/sct_e2e_gene.csv.gz").read() ==
+                                                        gzip.open("/tmp/sct_e2e_gene_host.csv.gz").read())
+        res["records"] = n
+        res["GatherGeneMetrics_records_per_s"] = n / min(runs)
     print(json.dumps(res))
 
 

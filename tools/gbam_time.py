@@ -15,6 +15,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("bam")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--mode", default="cell", choices=["cell", "gene"])
     a = ap.parse_args()
     import torch
 
@@ -26,7 +27,7 @@ def main():
     for _ in range(a.reps + 1):
         tm = {}
         t0 = time.perf_counter()
-        got = gbam.decode(a.bam, "cell", dev, timings=tm, lazy=True)
+        got = gbam.decode(a.bam, a.mode, dev, timings=tm, lazy=True)
         torch.cuda.synchronize()
         t = time.perf_counter() - t0
         if got is None:
