@@ -370,9 +370,17 @@ struct WelfordSide {
 
 int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent, const RecCols& rc2,
                   const int64_t* ent_start, double* out_f, hipStream_t s, WelfordSide& wf) {
-  HIPCHK(hipStreamCreateWithFlags(&wf.s2, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&wf.fork, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&wf.join, hipEventDisableTiming));
+  // the side stream lives on the caller's stream's device (the calling thread's current device
+  // may be another one)
+  int dev = 0, prev = 0;
+  HIPCHK(hipStreamGetDevice(s, &dev));
+  HIPCHK(hipGetDevice(&prev));
+  if (prev != dev) HIPCHK(hipSetDevice(dev));
+  hipError_t ce = hipStreamCreateWithFlags(&wf.s2, hipStreamNonBlocking);
+  if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.fork, hipEventDisableTiming);
+  if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.join, hipEventDisableTiming);
+  if (prev != dev) HIPCHK(hipSetDevice(prev));
+  HIPCHK(ce);
   HIPCHK(hipEventRecord(wf.fork, s));
   HIPCHK(hipStreamWaitEvent(wf.s2, wf.fork, 0));
   hipStream_t s2 = wf.s2;
