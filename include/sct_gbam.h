@@ -44,7 +44,17 @@ int sct_gbam_open(const char* path, int32_t device, void* stream, sct_gbam_t** o
  * Returns SCT_BAM_OK, SCT_GBAM_HOST, or SCT_BAM_EIO on a device error. */
 int sct_gbam_parse(sct_gbam_t* h, int32_t metric_mode, void* const* columns);
 
-/* The ranked dictionary `which` (SCT_BAM_TAG_CB / _UB / _GE) after sct_gbam_parse, as
+/* Phase 2, count-matrix mode (sct_bam.h SCT_BAM_COUNT_MATRIX; CountMatrix.from_sorted_tagged_bam,
+ * count.py:134-328): `tags` holds the cell, molecule and gene tag names (6 characters, as
+ * sct_bam_decode_tags); columns: cell, umi, gene (int32), xf (uint8: 0 no XF tag, 4 INTERGENIC,
+ * 5 any other value), qhead (uint8: 1 where the record's query name differs from the previous
+ * record's -- the itertools.groupby of count.py:83-86), each n_records elements.  No validation,
+ * as the reference reads only these tags.  A non-string value of a named tag returns
+ * SCT_GBAM_HOST (the host decoder applies the reference's str() or raises its error).
+ * Returns SCT_BAM_OK, SCT_GBAM_HOST, or SCT_BAM_EIO on a device error. */
+int sct_gbam_parse_count(sct_gbam_t* h, const char* tags, void* const* columns);
+
+/* The ranked dictionary `which` (SCT_BAM_TAG_CB / _UB / _GE) after sct_gbam_parse(_count), as
  * sct_bam_dictionary: *n names, names[i] = bytes[offsets[i] .. offsets[i+1]), entry 0 the
  * missing tag when *has_none.  Valid until sct_gbam_close. */
 int sct_gbam_dictionary(const sct_gbam_t* h, int32_t which, int64_t* n, const char** bytes,

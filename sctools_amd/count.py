@@ -2,8 +2,9 @@
 Count matrices -- same interface as the reference's ``sctools.count.CountMatrix``
 (``/root/reference/src/sctools/count.py:36-390``), built on the GPU.
 
-``from_sorted_tagged_bam`` decodes the BAM natively (``libsct_bam.so``, count-matrix mode:
-the three dictionary tags, XF and a query-name group flag per record) and counts on the
+``from_sorted_tagged_bam`` decodes the BAM on the GPU (``libsct_gbam.so``; a file it declines
+natively on the host, ``libsct_bam.so``), count-matrix mode: the three dictionary tags, XF and a
+query-name group flag per record, and counts on the
 device (``sct_count_matrix``, ``csrc/countmat.h``): one molecule key per query-name group,
 an LSD sort, distinct (cell, molecule, gene) triples summed per (cell, gene), rows ordered
 by each cell's first counted molecule -- the matrix, row index and column index of the
@@ -53,6 +54,18 @@ def _python_columns(path: str, open_mode: str, tags):
         "xf": np.asarray(xf, dtype=np.uint8), "qhead": np.asarray(qhead, dtype=np.uint8),
     }
     return arrays, [d.names for d in dicts]
+
+
+def _device_columns(path: str, open_mode: str, tags, dev):
+    """The count columns decoded on `dev` by libsct_gbam.so, or None (SAM, no device decoder, tag
+    names it cannot take, or a file it declines: typed tag values, non-ASCII strings ...)."""
+    from sctools_amd import gbam
+
+    if open_mode != "rb" or dev.type != "cuda" or not gbam.available():
+        return None
+    if any(len(t) != 2 or not t.isascii() or "\0" in t for t in tags):
+        return None
+    return gbam.decode(path, "count", device=dev, tags=tags)
 
 
 def gene_columns(gene_names: Sequence[Optional[str]], gene_name_to_index: Dict[str, int]) -> np.ndarray:
@@ -109,10 +122,13 @@ class CountMatrix:
         gene_name_tag: str = consts.GENE_NAME_TAG_KEY,
         open_mode: str = "rb",
         device=None,
+        gpu_decode: bool = True,
     ) -> "CountMatrix":
         """Cells x genes molecule counts of a query-name-grouped tagged BAM (count.py:134-328).
 
-        ``chromosomes_gene_locations_extended`` is accepted and, as in the reference, unused."""
+        ``chromosomes_gene_locations_extended`` is accepted and, as in the reference, unused.
+        A BAM is inflated and parsed on the counting device (``gbam``, count mode) unless
+        ``gpu_decode`` is False or the device decoder declines the file (then ``bamnative``)."""
         import torch
 
         from sctools_amd import bamnative, engine
@@ -120,17 +136,23 @@ class CountMatrix:
         tags = (cell_barcode_tag or consts.CELL_BARCODE_TAG_KEY,
                 molecule_barcode_tag or consts.MOLECULE_BARCODE_TAG_KEY,
                 gene_name_tag or consts.GENE_NAME_TAG_KEY)
-        try:
-            if open_mode != "rb":
-                raise bamnative.TypedTagValue("not BAM")
-            arrays, (cells, umis, genes) = bamnative.decode(bam_file, "count", tags=tags)
-        except bamnative.TypedTagValue:  # SAM, or float / array tag values: the Python reader
-            arrays, (cells, umis, genes) = _python_columns(bam_file, open_mode, tags)
-        gene_col = gene_columns(genes, gene_name_to_index)
         eng = engine.get_engine(device)
         dev = eng.device
+        got = _device_columns(bam_file, open_mode, tags, dev) if gpu_decode else None
+        if got is not None:  # decoded on the device: the columns are already in HBM
+            arrays, (cells, umis, genes) = got
+        else:
+            try:
+                if open_mode != "rb":
+                    raise bamnative.TypedTagValue("not BAM")
+                arrays, (cells, umis, genes) = bamnative.decode(bam_file, "count", tags=tags)
+            except bamnative.TypedTagValue:  # SAM, or float / array tag values: the Python reader
+                arrays, (cells, umis, genes) = _python_columns(bam_file, open_mode, tags)
+        gene_col = gene_columns(genes, gene_name_to_index)
 
         def put(a):
+            if isinstance(a, torch.Tensor):
+                return a
             return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
         n = int(arrays["cell"].shape[0])
@@ -144,7 +166,8 @@ class CountMatrix:
             max(1, len(umis)), 0 if cells and cells[0] is None else -1, 0 if umis and umis[0] is None else -1,
             len(gene_name_to_index))
         if unknown >= 0:
-            raise KeyError(_unknown_gene(arrays, genes, gene_col, unknown))
+            host = {c: (v.cpu().numpy() if isinstance(v, torch.Tensor) else v) for c, v in arrays.items()}
+            raise KeyError(_unknown_gene(host, genes, gene_col, unknown))
         row_cell, indptr, indices, data = (t.cpu().numpy() for t in res)
         n_rows = int(row_cell.shape[0])
         matrix = sp.csr_matrix((data.view(np.uint32), indices, indptr), shape=(n_rows, len(gene_name_to_index)))

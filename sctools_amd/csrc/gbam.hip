@@ -11,7 +11,8 @@
 //      every start by induction); a second walk writes the record offsets;
 //   4. k_parse: one lane per record -- the validation and fields of bamdec.cpp parse_record
 //      (sct_bam.h), and CB / UB / GE interned in open-addressing tables (one 64-bit CAS per
-//      insert: the string's offset in U, its length and 16 hash bits);
+//      insert: the string's offset in U, its length and 16 hash bits); k_parse_count: the
+//      count-matrix mode (three named tags, XF, the query-name group head);
 //   5. per dictionary the occupied slots are compacted, the distinct strings packed and copied to
 //      the host, sorted there (Python's sorted() order, the missing tag first) and the rank of
 //      every slot copied back; k_remap turns slot ids into ranks.
@@ -447,6 +448,74 @@ __global__ void k_parse(const uint8_t* __restrict__ U, const uint64_t* __restric
   if (host) atomicOr(&flags[0], 1u);
 }
 
+// One lane per record: bamdec.cpp parse_count_record (count.py:222-270 reads the three named
+// dictionary tags, XF and the query name; no validation) plus the itertools.groupby head flag of
+// count.py:83-86 -- the record's query name differs from the previous record's.  tags: the
+// three tag names as (a << 8 | b).
+struct CountCols {
+  int32_t *cell, *umi, *gene;
+  uint8_t *xf, *qhead;
+};
+__global__ void k_parse_count(const uint8_t* __restrict__ U, const uint64_t* __restrict__ starts, uint64_t n,
+                              uint32_t tcb, uint32_t tub, uint32_t tge, CountCols C, Dicts D,
+                              uint32_t* __restrict__ flags) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint64_t p = starts[r];
+  const uint32_t bs = u32(U, p);
+  const uint64_t d = p + 4;
+  bool host = false;
+  do {
+    if (bs < 32) { host = true; break; }
+    const uint32_t lrn = U[d + 8];
+    const uint32_t n_cigar = u16(U, d + 12);
+    const uint32_t l_seq = u32(U, d + 16);
+    const uint64_t tag0 = 32ull + lrn + 4ull * n_cigar + (l_seq + 1ull) / 2 + l_seq;
+    if (tag0 > bs || lrn == 0) { host = true; break; }
+    const uint64_t end = d + bs;
+    DTag cb{}, ub{}, ge{}, xf{};
+    uint64_t q = d + tag0;
+    while (q + 3 <= end) {
+      const uint32_t a = U[q], b = U[q + 1], t = U[q + 2];
+      q += 3;
+      DTag v{};
+      const uint32_t used = tag_value(U, q, end, t, &v);
+      if (!used) { host = true; break; }
+      q += used;
+      const uint32_t ab = a << 8 | b;
+      if (ab == tcb) cb = v;  // (not else-if: a tag name may be given twice, as on the host)
+      if (ab == tub) ub = v;
+      if (ab == tge) ge = v;
+      if (ab == ('X' << 8 | 'F')) xf = v;
+    }
+    if (host) break;
+    if ((cb.kind && cb.kind != TV_STR) || (ub.kind && ub.kind != TV_STR) || (ge.kind && ge.kind != TV_STR)) {
+      host = true;  // integer / float / array values: the host's str() of them, or its ETYPED
+      break;
+    }
+    uint32_t x = XF_ABSENT;
+    if (xf.kind) x = xf.kind == TV_STR && lit_eq(U, xf, "INTERGENIC", 10) ? XF_INTERGENIC : XF_OTHER;
+    uint32_t head = 1;
+    if (r) {
+      const uint64_t pp = starts[r - 1] + 4;
+      // the previous record's name lies before this record (a malformed previous record sets
+      // *host on its own lane, and then head is not used)
+      if (U[pp + 8] == lrn && pp + 32 + lrn <= p) head = !str_eq(U, pp + 32, d + 32, lrn - 1);
+    }
+    int32_t id0 = -1, id1 = -1, id2 = -1;
+    if (cb.kind) host |= (id0 = intern(D.table[0], D.mask[0], U, cb.off, cb.n)) < 0;
+    else atomicOr(&flags[1], 1u);
+    if (ub.kind) host |= (id1 = intern(D.table[1], D.mask[1], U, ub.off, ub.n)) < 0;
+    else atomicOr(&flags[2], 1u);
+    if (ge.kind) host |= (id2 = intern(D.table[2], D.mask[2], U, ge.off, ge.n)) < 0;
+    else atomicOr(&flags[3], 1u);
+    if (host) break;
+    C.cell[r] = id0, C.umi[r] = id1, C.gene[r] = id2;
+    C.xf[r] = (uint8_t)x, C.qhead[r] = (uint8_t)head;
+  } while (false);
+  if (host) atomicOr(&flags[0], 1u);
+}
+
 // ---------------- dictionaries ----------------
 __global__ void k_occupied(const unsigned long long* __restrict__ table, uint64_t cap, uint32_t* __restrict__ occ) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -786,46 +855,51 @@ int open_impl(const char* path, int32_t device, void* stream, sct_gbam_t** out, 
   return SCT_BAM_OK;
 }
 
-int parse_impl(sct_gbam* G, int32_t metric_mode, void* const* cols) {
-  const double t0 = now();
-  HIPOK(hipSetDevice(G->device));
-  hipStream_t st = G->st;
-  const uint64_t n = (uint64_t)G->n;
+// The three device hash tables (2n slots each, a power of two) and the parse flags: [0] a record
+// needs the host decoder, [1..3] some record lacks CB / UB / GE.
+struct ParseState {
   uint64_t cap = 1024;
-  while (cap < 2 * n) cap <<= 1;
-  if (cap > (1ull << 31)) return gfail(SCT_GBAM_HOST, "too many records for the device tables");
   DevBuf<unsigned long long> tab[3];
   Dicts D;
-  for (int k = 0; k < 3; k++) {
-    HIPOK(tab[k].alloc(cap));
-    HIPOK(hipMemsetAsync(tab[k].p, 0, cap * sizeof(unsigned long long), st));
-    D.table[k] = tab[k].p;
-    D.mask[k] = cap - 1;
-  }
   DevBuf<uint32_t> flags;
-  HIPOK(flags.alloc(4));
-  HIPOK(hipMemsetAsync(flags.p, 0, 4 * sizeof(uint32_t), st));
-  Cols C;
-  C.cell = (int32_t*)cols[0], C.umi = (int32_t*)cols[1], C.gene = (int32_t*)cols[2];
-  C.ref = (int32_t*)cols[3], C.pos = (int32_t*)cols[4];
-  C.gq_sum = (uint16_t*)cols[5], C.gq_len = (uint16_t*)cols[6], C.gq_gt30 = (uint16_t*)cols[7];
-  C.bits = (uint8_t*)cols[8], C.xf = (uint8_t*)cols[9], C.cy_gt30 = (uint8_t*)cols[10];
-  C.cy_len = (uint8_t*)cols[11], C.uy_gt30 = (uint8_t*)cols[12], C.uy_len = (uint8_t*)cols[13];
-  hipLaunchKernelGGL(k_parse, dim3(grid(n, 256)), dim3(256), 0, st, G->u.p, G->starts.p, n,
-                     metric_mode == SCT_BAM_CELL_METRICS ? 1u : 0u, C, D, flags.p);
-  HIPOK(hipGetLastError());
-  uint32_t fl[4];
-  HIPOK(hipMemcpyAsync(fl, flags.p, sizeof(fl), hipMemcpyDeviceToHost, st));
-  HIPOK(hipStreamSynchronize(st));
-  G->t[4] = now() - t0;
-  if (fl[0]) return gfail(SCT_GBAM_HOST, "a record needs the host decoder");
+  uint32_t fl[4] = {0, 0, 0, 0};
+};
 
+int parse_begin(sct_gbam* G, ParseState& P) {
+  HIPOK(hipSetDevice(G->device));
+  const uint64_t n = (uint64_t)G->n;
+  while (P.cap < 2 * n) P.cap <<= 1;
+  if (P.cap > (1ull << 31)) return gfail(SCT_GBAM_HOST, "too many records for the device tables");
+  for (int k = 0; k < 3; k++) {
+    HIPOK(P.tab[k].alloc(P.cap));
+    HIPOK(hipMemsetAsync(P.tab[k].p, 0, P.cap * sizeof(unsigned long long), G->st));
+    P.D.table[k] = P.tab[k].p;
+    P.D.mask[k] = P.cap - 1;
+  }
+  HIPOK(P.flags.alloc(4));
+  HIPOK(hipMemsetAsync(P.flags.p, 0, 4 * sizeof(uint32_t), G->st));
+  return SCT_BAM_OK;
+}
+
+int parse_flags(sct_gbam* G, ParseState& P) {
+  HIPOK(hipGetLastError());
+  HIPOK(hipMemcpyAsync(P.fl, P.flags.p, sizeof(P.fl), hipMemcpyDeviceToHost, G->st));
+  HIPOK(hipStreamSynchronize(G->st));
+  if (P.fl[0]) return gfail(SCT_GBAM_HOST, "a record needs the host decoder");
+  return SCT_BAM_OK;
+}
+
+// The interned ids -> ranks in Python's sorted() order (None first), and the ranked strings.
+int dictionaries_impl(sct_gbam* G, ParseState& P, int32_t* const colk[3]) {
   const double t1 = now();
+  hipStream_t st = G->st;
+  const uint64_t n = (uint64_t)G->n, cap = P.cap;
+  const uint32_t* fl = P.fl;
+  DevBuf<unsigned long long>* tab = P.tab;
   DevBuf<uint32_t> occ, dense;
   DevBuf<uint8_t> tmp;
   HIPOK(occ.alloc(cap));
   HIPOK(dense.alloc(cap));
-  int32_t* colk[3] = {C.cell, C.umi, C.gene};
   for (int k = 0; k < 3; k++) {
     const int32_t hn = fl[1 + k] ? 1 : 0;
     G->has_none[k] = hn;
@@ -882,6 +956,46 @@ int parse_impl(sct_gbam* G, int32_t metric_mode, void* const* cols) {
   return SCT_BAM_OK;
 }
 
+int parse_impl(sct_gbam* G, int32_t metric_mode, void* const* cols) {
+  const double t0 = now();
+  ParseState P;
+  int rc = parse_begin(G, P);
+  if (rc) return rc;
+  const uint64_t n = (uint64_t)G->n;
+  Cols C;
+  C.cell = (int32_t*)cols[0], C.umi = (int32_t*)cols[1], C.gene = (int32_t*)cols[2];
+  C.ref = (int32_t*)cols[3], C.pos = (int32_t*)cols[4];
+  C.gq_sum = (uint16_t*)cols[5], C.gq_len = (uint16_t*)cols[6], C.gq_gt30 = (uint16_t*)cols[7];
+  C.bits = (uint8_t*)cols[8], C.xf = (uint8_t*)cols[9], C.cy_gt30 = (uint8_t*)cols[10];
+  C.cy_len = (uint8_t*)cols[11], C.uy_gt30 = (uint8_t*)cols[12], C.uy_len = (uint8_t*)cols[13];
+  hipLaunchKernelGGL(k_parse, dim3(grid(n, 256)), dim3(256), 0, G->st, G->u.p, G->starts.p, n,
+                     metric_mode == SCT_BAM_CELL_METRICS ? 1u : 0u, C, P.D, P.flags.p);
+  rc = parse_flags(G, P);
+  G->t[4] = now() - t0;
+  if (rc) return rc;
+  int32_t* const colk[3] = {C.cell, C.umi, C.gene};
+  return dictionaries_impl(G, P, colk);
+}
+
+int parse_count_impl(sct_gbam* G, const char* tags, void* const* cols) {
+  const double t0 = now();
+  ParseState P;
+  int rc = parse_begin(G, P);
+  if (rc) return rc;
+  const uint64_t n = (uint64_t)G->n;
+  CountCols C;
+  C.cell = (int32_t*)cols[0], C.umi = (int32_t*)cols[1], C.gene = (int32_t*)cols[2];
+  C.xf = (uint8_t*)cols[3], C.qhead = (uint8_t*)cols[4];
+  auto tag = [&](int k) { return (uint32_t)(uint8_t)tags[2 * k] << 8 | (uint8_t)tags[2 * k + 1]; };
+  hipLaunchKernelGGL(k_parse_count, dim3(grid(n, 256)), dim3(256), 0, G->st, G->u.p, G->starts.p, n, tag(0),
+                     tag(1), tag(2), C, P.D, P.flags.p);
+  rc = parse_flags(G, P);
+  G->t[4] = now() - t0;
+  if (rc) return rc;
+  int32_t* const colk[3] = {C.cell, C.umi, C.gene};
+  return dictionaries_impl(G, P, colk);
+}
+
 }  // namespace
 
 extern "C" {
@@ -904,6 +1018,16 @@ int sct_gbam_parse(sct_gbam_t* h, int32_t metric_mode, void* const* columns) {
   for (int k = 0; k < 14; k++)
     if (!columns[k]) return gfail(SCT_BAM_EIO, "NULL column");
   return parse_impl(h, metric_mode, columns);
+}
+
+int sct_gbam_parse_count(sct_gbam_t* h, const char* tags, void* const* columns) {
+  g_gerr.clear();
+  if (!h || !tags || !columns) return gfail(SCT_BAM_EIO, "NULL argument");
+  for (int k = 0; k < 6; k++)
+    if (!tags[k]) return gfail(SCT_BAM_EIO, "tags: six characters (cell, molecule, gene tag names)");
+  for (int k = 0; k < 5; k++)
+    if (!columns[k]) return gfail(SCT_BAM_EIO, "NULL column");
+  return parse_count_impl(h, tags, columns);
 }
 
 int sct_gbam_dictionary(const sct_gbam_t* h, int32_t which, int64_t* n, const char** bytes, const int64_t** offsets,

@@ -24,7 +24,7 @@ LIB_PATH = os.environ.get("SCT_GBAM_LIB_PATH") or os.path.join(HERE, "libsct_gba
 
 OK, HOST = 0, 1
 _MODES = {"cell": 0, "gene": 1}
-EXPORTED = ("sct_gbam_open", "sct_gbam_parse", "sct_gbam_dictionary", "sct_gbam_read_inflated", "sct_gbam_timing",
+EXPORTED = ("sct_gbam_open", "sct_gbam_parse", "sct_gbam_parse_count", "sct_gbam_dictionary", "sct_gbam_read_inflated", "sct_gbam_timing",
             "sct_gbam_close", "sct_gbam_last_error")
 STAGES = ("map_scan", "h2d", "inflate", "record_starts", "parse_intern", "dictionaries", "members",
           "start_rounds")
@@ -48,6 +48,8 @@ def load() -> ctypes.CDLL:
     L.sct_gbam_open.argtypes = [ctypes.c_char_p, i32, vp, ctypes.POINTER(vp), ctypes.POINTER(i64)]
     L.sct_gbam_parse.restype = ctypes.c_int
     L.sct_gbam_parse.argtypes = [vp, i32, ctypes.POINTER(vp)]
+    L.sct_gbam_parse_count.restype = ctypes.c_int
+    L.sct_gbam_parse_count.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
     L.sct_gbam_dictionary.restype = ctypes.c_int
     L.sct_gbam_dictionary.argtypes = [vp, i32, ctypes.POINTER(i64), ctypes.POINTER(vp), ctypes.POINTER(vp),
                                       ctypes.POINTER(i32)]
@@ -96,11 +98,17 @@ def _check(rc: int):
         raise OSError("device BAM decode failed (%d): %s" % (rc, last_error()))
 
 
+COUNT_COLUMNS = ("cell", "umi", "gene", "xf", "qhead")
+
+
 def decode(path: str, metric_mode: str = "cell", device=None, timings: Optional[dict] = None,
-           lazy: bool = False):
+           lazy: bool = False, tags=None):
     """(device column tensors, [cell names, umi names, gene names]) -- or None when the file needs
     the host decoder.  Names in id order, None first when a record lacks the tag; with ``lazy``
-    each dictionary is a ``columnar.PackedDictionary`` (strings decoded only when asked for)."""
+    each dictionary is a ``columnar.PackedDictionary`` (strings decoded only when asked for).
+
+    ``metric_mode`` "count": the count-matrix columns ``COUNT_COLUMNS`` of the three tags named by
+    ``tags`` (cell, molecule, gene), as ``bamnative.decode(path, "count", tags=tags)``."""
     import torch
 
     from sctools_amd import _native as N
@@ -111,9 +119,17 @@ def decode(path: str, metric_mode: str = "cell", device=None, timings: Optional[
         _check(H.rc)
         if H.rc == HOST:
             return None
-        cols = {c: torch.empty(H.n, dtype=_TORCH_DTYPES[c], device=H.dev) for c in N.RECORD_COLUMNS}
-        ptrs = (ctypes.c_void_p * len(N.RECORD_COLUMNS))(*[cols[c].data_ptr() for c in N.RECORD_COLUMNS])
-        rc = H.L.sct_gbam_parse(H.h, _MODES[metric_mode], ptrs)
+        if metric_mode == "count":
+            if tags is None or len(tags) != 3 or any(len(t) != 2 for t in tags):
+                raise ValueError("count mode needs three 2-character tag names")
+            cols = {c: torch.empty(H.n, dtype=torch.int32 if c in ("cell", "umi", "gene") else torch.uint8,
+                                   device=H.dev) for c in COUNT_COLUMNS}
+            ptrs = (ctypes.c_void_p * len(COUNT_COLUMNS))(*[cols[c].data_ptr() for c in COUNT_COLUMNS])
+            rc = H.L.sct_gbam_parse_count(H.h, "".join(tags).encode("ascii"), ptrs)
+        else:
+            cols = {c: torch.empty(H.n, dtype=_TORCH_DTYPES[c], device=H.dev) for c in N.RECORD_COLUMNS}
+            ptrs = (ctypes.c_void_p * len(N.RECORD_COLUMNS))(*[cols[c].data_ptr() for c in N.RECORD_COLUMNS])
+            rc = H.L.sct_gbam_parse(H.h, _MODES[metric_mode], ptrs)
         _check(rc)
         if rc == HOST:
             return None

@@ -150,9 +150,13 @@ def main():
                     help="GatherGeneMetrics on a gene-sorted BAM (small-gene-sorted.bam, each record "
                          "repeated --records-per-run times, gene names renamed per replica) instead")
     ap.add_argument("--records-per-run", type=int, default=20)
+    ap.add_argument("--count", action="store_true",
+                    help="CountMatrix.from_sorted_tagged_bam (CreateCountMatrix) on the cell-sorted BAM instead")
     a = ap.parse_args()
     if a.gene:
         return main_gene(a)
+    if a.count:
+        return main_count(a)
     bam = a.bam or "/tmp/sct_e2e_%d.bam" % a.records
     if not os.path.exists(bam):
         t0 = time.time()
@@ -253,6 +257,48 @@ def main_gene(a):
                                                         gzip.open("/tmp/sct_e2e_gene_host.csv.gz").read())
         res["records"] = n
         res["GatherGeneMetrics_records_per_s"] = n / min(runs)
+    print(json.dumps(res))
+
+
+def main_count(a):
+    """CountMatrix.from_sorted_tagged_bam end to end: device decode (count mode) + GPU counting,
+    against the same call with the host decoder; the gene index is every GE value of the file."""
+    bam = a.bam or "/tmp/sct_e2e_%d.bam" % a.records
+    if not os.path.exists(bam):
+        make_bam(bam, a.records, a.replicas_per_cell)
+    import numpy as np
+    import torch
+
+    from sctools_amd import bamnative
+    from sctools_amd import count as C
+
+    torch.cuda.init()
+    with open(bam, "rb") as f:
+        while f.read(1 << 26):
+            pass
+    arrays, (_, _, genes) = bamnative.decode(bam, "count", tags=("CB", "UB", "GE"))
+    n = int(arrays["cell"].shape[0])
+    names = {g: i for i, g in enumerate(sorted(g for g in genes if g is not None and "," not in g))}
+    res = {"bam": bam, "bam_mb": os.path.getsize(bam) / 1e6, "entry": "CountMatrix.from_sorted_tagged_bam",
+           "records": n, "genes": len(names)}
+    C.CountMatrix.from_sorted_tagged_bam(bam, names, device="cuda:0")  # warm-up
+    torch.cuda.synchronize()
+    runs = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        m = C.CountMatrix.from_sorted_tagged_bam(bam, names, device="cuda:0")
+        runs.append(time.perf_counter() - t0)
+    res["device_decode_s"] = runs
+    res["records_per_s"] = n / min(runs)
+    res["nnz"] = int(m.matrix.nnz)
+    if a.host_decoder:
+        t0 = time.perf_counter()
+        h = C.CountMatrix.from_sorted_tagged_bam(bam, names, device="cuda:0", gpu_decode=False)
+        res["host_decoder_s"] = time.perf_counter() - t0
+        res["host_decoder_records_per_s"] = n / res["host_decoder_s"]
+        res["device_and_host_decoder_identical"] = bool(
+            m.matrix.shape == h.matrix.shape and (m.matrix != h.matrix).nnz == 0
+            and np.array_equal(m.row_index, h.row_index))
     print(json.dumps(res))
 
 
