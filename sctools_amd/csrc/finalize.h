@@ -92,7 +92,8 @@ struct Welford {
 //     within 2^-104 of delta / k, which is never that close to a rounding midpoint unless it is a
 //     double, so q = RN(delta / k) (tests/native/welfdiv.c checks it against IEEE division) and
 //     each update is bit-identical to Python's.  The longest entity's chain bounds the time: 4
-//     dependent FP64 operations per record (sub, mul, fma, add), no memory or LDS latency on it.
+//     dependent FP64 operations per record (sub, mul, fma, add), no memory or LDS latency on it,
+//     with the M2 update of each record issued beside the next record's chain.
 constexpr int kWfWave = 48;  // records from which an entity gets a wave of its own
 constexpr int kWfBins = 32;  // log2 size classes
 struct WelfordCtl {
@@ -229,6 +230,9 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
     const int64_t clen = mine ? len : kmax;
     const int64_t lastx = clen > 0 ? clen - 1 : 0;
     double mean = 0.0, m2 = 0.0;
+    // the pending M2 term of the last record updated (zeros add exactly 0.0 to m2 = 0.0)
+    double pdelta = 0.0, px = 0.0;
+    bool pact = true;
     double xb[kWfBatch], xn[kWfBatch];
 #pragma unroll
     for (int q = 0; q < kWfBatch; q++) xb[q] = X[4 * (q < lastx ? q : lastx)];
@@ -257,28 +261,44 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
             }
           }
         }
-        const auto update = [&](int q, bool act) {
-          const double delta = xb[q] - mean;
+        // Record q's M2 term (x_q - mean_q) delta_q runs at record q + 1, beside its mean chain:
+        // waves issue in order, and after the mean add the M2 sub -> mul -> add would otherwise hold
+        // the next record's ops behind two more dependent FP64 latencies (12.9 against 14.3 ms
+        // at config 2, profiles/r03/s_welford_m2_pipelined/).  Same operations on the same values.
+        const auto update = [&](int q, bool act, bool fast) {
+          const double x = xb[q];
           const double h = readlane_f64(yh, hb * kWfBatch + q), l = readlane_f64(yl, hb * kWfBatch + q);
-          const double nm = mean + __fma_rn(delta, h, delta * l);  // + RN(delta / k)
-          const double delta2 = xb[q] - nm;
-          const double nm2 = m2 + delta * delta2;
+          // the issue order is pinned by empty asm statements (the scheduler would put the M2 ops
+          // back between two records): the two subs, the two muls, the fma and the M2 add, then
+          // the mean add
+          double delta = x - mean;
+          double d2 = px - mean;
+          asm volatile("" : "+v"(delta), "+v"(d2));
+          double t = delta * l;
+          double p2 = pdelta * d2;
+          asm volatile("" : "+v"(t), "+v"(p2));
+          double f = __fma_rn(delta, h, t);  // RN(delta / k)
+          double pm2 = m2 + p2;
+          asm volatile("" : "+v"(f), "+v"(pm2));
+          m2 = fast || pact ? pm2 : m2;
+          const double nm = mean + f;
           mean = act ? nm : mean;
-          m2 = act ? nm2 : m2;
+          pdelta = delta, px = x, pact = act;
         };
         // no lane-divergent branch around the updates: readlane must see y of every lane (a
         // value computed under a partial exec mask would be stale in the inactive lanes)
         if (__builtin_amdgcn_ballot_w64(c + kWfBatch > clen) == 0) {  // wave-uniform
 #pragma unroll
-          for (int q = 0; q < kWfBatch; q++) update(q, true);
+          for (int q = 0; q < kWfBatch; q++) update(q, true, true);
         } else {
 #pragma unroll
-          for (int q = 0; q < kWfBatch; q++) update(q, c + q < clen);
+          for (int q = 0; q < kWfBatch; q++) update(q, c + q < clen, false);
         }
 #pragma unroll
         for (int q = 0; q < kWfBatch; q++) xb[q] = xn[q];
       }
     }
+    m2 = pact ? m2 + pdelta * (px - mean) : m2;  // the last record's pending M2 term
     if (mine) {
       double* F = out_f + e * SCT_NF;
       welford_store<kCell>(F, st, mean, m2, len);
