@@ -9,10 +9,16 @@ BAMDEC := sctools_amd/libsct_bam.so
 CSVFMT := sctools_amd/libsct_csv.so
 GBAM := sctools_amd/libsct_gbam.so
 
-all: $(ENGINE) $(BAMDEC) $(CSVFMT) $(GBAM) oracle/liboracle.so tests/native/libfxcheck.so
+SI4 := tests/native/libsct_engine_si4.so
+
+all: $(ENGINE) $(BAMDEC) $(CSVFMT) $(GBAM) oracle/liboracle.so tests/native/libfxcheck.so $(SI4)
 
 $(ENGINE): $(SRC) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC) -L/opt/rocm/lib -lrccl
+
+# test infrastructure: the engine with 1024-item radix tiles (tests/test_gpu_tagsort.py)
+$(SI4): $(SRC) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -DSCT_SORT_ITEMS=4 -o $@ $(SRC) -L/opt/rocm/lib -lrccl
 
 $(BAMDEC): sctools_amd/csrc/bamdec.cpp sctools_amd/csrc/bamsplit.cpp sctools_amd/csrc/bgzf.h include/sct_bam.h
 	g++ -O3 -std=c++17 -fopenmp -fPIC -shared -Wall -o $@ sctools_amd/csrc/bamdec.cpp sctools_amd/csrc/bamsplit.cpp -lz
@@ -30,6 +36,6 @@ tests/native/libfxcheck.so: tests/native/fxcheck.cpp sctools_amd/csrc/fixedpt.h
 	g++ -O2 -std=c++17 -ffp-contract=off -fPIC -shared -o $@ tests/native/fxcheck.cpp
 
 clean:
-	rm -f $(ENGINE) $(BAMDEC) $(CSVFMT) $(GBAM) oracle/liboracle.so tests/native/libfxcheck.so
+	rm -f $(ENGINE) $(BAMDEC) $(CSVFMT) $(GBAM) oracle/liboracle.so tests/native/libfxcheck.so $(SI4)
 
 .PHONY: all clean

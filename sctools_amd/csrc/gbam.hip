@@ -25,6 +25,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <hipcub/hipcub.hpp>
 #include <memory>
@@ -561,27 +562,67 @@ int gfail(int code, const char* msg) {
   return code;
 }
 
-#define HIPOK(x)                                          \
-  do {                                                    \
-    hipError_t e_ = (x);                                  \
-    if (e_ != hipSuccess) return gfail(SCT_BAM_EIO, hipGetErrorString(e_)); \
+// A device allocation that fails declines the file to the host decoder (SCT_GBAM_HOST) instead of
+// failing the decode: a BAM too large for the device's memory is still a valid input.
+#define HIPOK(x)                                                                            \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ == hipErrorOutOfMemory) {                                                        \
+      (void)hipGetLastError();                                                              \
+      return gfail(SCT_GBAM_HOST, "device memory exhausted: the host decoder takes the file"); \
+    }                                                                                       \
+    if (e_ != hipSuccess) return gfail(SCT_BAM_EIO, hipGetErrorString(e_));                 \
   } while (0)
+
+// SCT_GBAM_MAX_DEVICE_BYTES (tests): a cap on the device bytes the process's decodes hold at once;
+// an allocation past it fails as hipMalloc does when HBM is exhausted.
+uint64_t device_cap() {  // read per allocation (a few per decode): tests change it between calls
+  const char* v = getenv("SCT_GBAM_MAX_DEVICE_BYTES");
+  return v && *v ? (uint64_t)strtoull(v, nullptr, 10) : ~0ull;
+}
+std::atomic<uint64_t> g_held{0};  // device bytes held by DevBufs
 
 template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  size_t bytes = 0;
   hipError_t alloc(size_t count) {
     free();
+    const size_t b = std::max<size_t>(count, 1) * sizeof(T);
+    if (g_held + b > device_cap()) return hipErrorOutOfMemory;
+    const hipError_t e = hipMalloc(&p, b);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
     n = count;
-    return hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
+    bytes = b;
+    g_held += b;
+    return hipSuccess;
   }
   void free() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      (void)hipFree(p);
+      g_held -= bytes;
+    }
     p = nullptr;
     n = 0;
+    bytes = 0;
   }
   ~DevBuf() { free(); }
+};
+
+// the caller thread's current device, restored when an entry point returns (the library switches to
+// the handle's device; the caller's own work must not move with it)
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
 };
 
 // the byte offset where the alignments start: magic, l_text, text, n_ref, references
@@ -671,13 +712,14 @@ namespace {
 template <class I, class O>
 hipError_t exclusive_sum(I* in, O* out, uint64_t n, hipStream_t st, DevBuf<uint8_t>& tmp) {
   size_t bytes = 0;
-  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n, st);
+  // 64-bit item counts (rocPRIM scans size_t items): parse_begin admits tables of 2^31 slots
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (size_t)n, st);
   if (e != hipSuccess) return e;
   if (tmp.n < bytes) {
     e = tmp.alloc(bytes);
     if (e != hipSuccess) return e;
   }
-  return hipcub::DeviceScan::ExclusiveSum(tmp.p, bytes, in, out, (int)n, st);
+  return hipcub::DeviceScan::ExclusiveSum(tmp.p, bytes, in, out, (size_t)n, st);
 }
 
 inline unsigned grid(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
@@ -1007,6 +1049,7 @@ int sct_gbam_open(const char* path, int32_t device, void* stream, sct_gbam_t** o
   if (out) *out = nullptr;
   if (n_records) *n_records = 0;
   if (!path || !out || !n_records) return gfail(SCT_BAM_EIO, "NULL argument");
+  DeviceGuard guard;
   return open_impl(path, device, stream, out, n_records);
 }
 
@@ -1017,6 +1060,7 @@ int sct_gbam_parse(sct_gbam_t* h, int32_t metric_mode, void* const* columns) {
     return gfail(SCT_BAM_EIO, "the device decode reads the cell and gene metric modes");
   for (int k = 0; k < 14; k++)
     if (!columns[k]) return gfail(SCT_BAM_EIO, "NULL column");
+  DeviceGuard guard;
   return parse_impl(h, metric_mode, columns);
 }
 
@@ -1027,6 +1071,7 @@ int sct_gbam_parse_count(sct_gbam_t* h, const char* tags, void* const* columns) 
     if (!tags[k]) return gfail(SCT_BAM_EIO, "tags: six characters (cell, molecule, gene tag names)");
   for (int k = 0; k < 5; k++)
     if (!columns[k]) return gfail(SCT_BAM_EIO, "NULL column");
+  DeviceGuard guard;
   return parse_count_impl(h, tags, columns);
 }
 
@@ -1045,6 +1090,7 @@ int sct_gbam_read_inflated(const sct_gbam_t* h, uint64_t off, uint64_t n, void* 
   if (total) *total = h->ulen;
   if (!n) return SCT_BAM_OK;
   if (!dst || off > h->ulen || n > h->ulen - off) return gfail(SCT_BAM_EIO, "range outside the payload");
+  DeviceGuard guard;
   HIPOK(hipSetDevice(h->device));
   HIPOK(hipMemcpy(dst, h->u.p + off, n, hipMemcpyDeviceToHost));
   return SCT_BAM_OK;
@@ -1058,6 +1104,7 @@ int sct_gbam_timing(const sct_gbam_t* h, double* t8) {
 
 void sct_gbam_close(sct_gbam_t* h) {
   if (!h) return;
+  DeviceGuard guard;
   (void)hipSetDevice(h->device);
   delete h;
 }

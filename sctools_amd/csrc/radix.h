@@ -15,7 +15,13 @@ namespace sct {
 constexpr int kItems = 16;
 constexpr int kTile = kBlock * kItems;  // 4096 records per tile (entity-run heads, key pass)
 // LSD radix sort tiles: 2048 items (24 KB of keys / values staged in LDS, so 6 blocks fit a CU)
-constexpr int kSortItems = 8;  // 12 / 16 items (3072 / 4096-item tiles, 2 blocks per CU): config 5 20.3 / 21.9 ms vs 19.7
+// 12 / 16 items (3072 / 4096-item tiles, 2 blocks per CU): config 5 20.3 / 21.9 ms vs 19.7.  The
+// macro exists for tests/native/libsct_engine_si4.so (1024-item tiles: the tiling that exposed the
+// round-3 tag-sort workspace bug, tests/test_gpu_tagsort.py::test_tag_sort_small_radix_tiles).
+#ifndef SCT_SORT_ITEMS
+#define SCT_SORT_ITEMS 8
+#endif
+constexpr int kSortItems = SCT_SORT_ITEMS;
 constexpr int kSortTile = kBlock * kSortItems;
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
@@ -138,14 +144,18 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __re
 struct SortBuffers {
   uint64_t *ka, *kb;
   uint32_t *va, *vb;
-  uint32_t *counts, *offsets;  // kRadix * cdiv(n, kSortTile) each
-  uint64_t* sums;              // cdiv(kRadix * tiles, kScanChunk)
+  uint32_t *counts, *offsets;  // count_cap entries each (>= kRadix * cdiv(n, kSortTile))
+  uint64_t* sums;              // cdiv(count_cap, kScanChunk) + 1
+  int64_t count_cap;
 };
 
 // LSD sort of (ka, va) over the low `bits` bits; *which = 0 if the result is in (ka, va), 1 if in (kb, vb)
 inline int radix_sort(const SortBuffers& B, int64_t n, int bits, int* which, hipStream_t s) {
   const int passes = (bits + kRadixBits - 1) / kRadixBits;
   const int64_t tiles = cdiv(n, kSortTile);
+  if ((int64_t)kRadix * tiles > B.count_cap)  // (the round-3 tag-sort layout violated this)
+    return fail(SCT_EINVAL, "radix_sort: %lld digit counts exceed the workspace's %lld", (long long)(kRadix * tiles),
+                (long long)B.count_cap);
   int cur = 0;
   for (int ps = 0; ps < passes; ps++) {
     const int shift = ps * kRadixBits;

@@ -48,7 +48,7 @@ struct Layout {
   size_t tile_cnt, scalars, scan_sums, pay_a, pay_b, half, counts, offsets, ent_start, partials;
   size_t gcounts, gcursor, gtoff, gwork, dflags, gpay, seen, zero_mito, ent_hist, l1_toff, l1_tslot;
   size_t bdesc, bent, seg_a, seg_b, work_a, work_b, seg_hist, seg_cur, giants, bigs, wctl, worder, wx, total;
-  int64_t num_tiles, num_chunks, max_ent, max_gene_work, max_seg, max_work;
+  int64_t num_tiles, num_chunks, max_ent, max_gene_work, max_seg, max_work, count_cap;
   int n_buckets;
   bool gene;
 };
@@ -60,6 +60,7 @@ Layout layout_for(const sct_plan_t* plan) {
   L.num_tiles = cdiv(n1, kTile);
   const int64_t m = (int64_t)kRadix * cdiv(n1, kSortTile);  // radix counts of the global-sort path
   L.num_chunks = cdiv(m, kScanChunk);
+  L.count_cap = m;
   L.max_ent = plan->max_entities > 0 ? plan->max_entities : n1;
   L.gene = plan->mode == SCT_MODE_GENE_GROUPED || (plan->flags & SCT_PLAN_GENE_PARTIALS);
   L.n_buckets = (int)cdiv(plan->n_gene_ids > 0 ? plan->n_gene_ids : 1, kGenesPerBucket);
@@ -467,7 +468,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
               rec->cy_gt30, rec->cy_len, rec->uy_gt30, rec->uy_len};
   SortBuffers B{at<uint64_t>(ws, L.pay_a), at<uint64_t>(ws, L.pay_b), at<uint32_t>(ws, L.pay_a + L.half),
                 at<uint32_t>(ws, L.pay_b + L.half), at<uint32_t>(ws, L.counts), at<uint32_t>(ws, L.offsets),
-                at<uint64_t>(ws, L.scan_sums)};
+                at<uint64_t>(ws, L.scan_sums), L.count_cap};
   int64_t* ent_start = at<int64_t>(ws, L.ent_start);
   int64_t* partials = at<int64_t>(ws, L.partials);
   uint32_t* gcounts = gene ? at<uint32_t>(ws, L.gcounts) : nullptr;
@@ -590,11 +591,13 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
 // ---- tag sort ----
 struct SortLayout {
   size_t recs, recs2, ka, kb, va, vb, counts, offsets, sums, bad, lka, lkb, lva, lvb, longs, tctl, total;
+  int64_t count_cap;
 };
 
 struct CountLayout {
   size_t ka, kb, va, vb, counts, offsets, sums, flags_a, offs_a, flags_b, offs_b, pair_cell, pair_col, pair_tri;
   size_t cell_first, cell_npairs, cell_pstart, row_of, row_pairs, scalars, total;
+  int64_t count_cap;
 };
 
 CountLayout count_layout(const sct_count_input_t* in) {
@@ -603,6 +606,7 @@ CountLayout count_layout(const sct_count_input_t* in) {
   const int64_t c1 = in->n_cell_ids > 0 ? in->n_cell_ids : 1;
   const int64_t m = n1 > c1 ? n1 : c1;  // the record sort and the cell-order sort share buffers
   const int64_t cm = (int64_t)kRadix * cdiv(m, kSortTile);
+  L.count_cap = cm;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -636,8 +640,15 @@ CountLayout count_layout(const sct_count_input_t* in) {
 SortLayout sort_layout(int64_t n) {
   SortLayout L;
   const int64_t n1 = n > 0 ? n : 1;
-  const int64_t tiles = cdiv(n1, kRowTile);  // row passes use the smaller tiles
+  // The digit counts serve two tilings: the row passes (kRowTile) and radix_sort (kSortTile, the
+  // tiebreak and multi-round paths).  Round 3 sized them by kRowTile alone, which only held while
+  // both tiles were 2048 items: a 1024-item kSortTile overflowed `counts` into `offsets`, the scan
+  // then read its own output, and the downsweep wrote through garbage offsets (the illegal memory
+  // access of the SCT_SORT_ITEMS=4 build).  radix_sort now also checks its capacity.
+  const int64_t row_tiles = cdiv(n1, kRowTile), sort_tiles = cdiv(n1, kSortTile);
+  const int64_t tiles = row_tiles > sort_tiles ? row_tiles : sort_tiles;
   const int64_t m = (int64_t)kRadix * tiles;
+  L.count_cap = m;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -897,7 +908,7 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
   }
   SortBuffers B{at<uint64_t>(workspace, L.ka), at<uint64_t>(workspace, L.kb), at<uint32_t>(workspace, L.va),
                 at<uint32_t>(workspace, L.vb), at<uint32_t>(workspace, L.counts), at<uint32_t>(workspace, L.offsets),
-                at<uint64_t>(workspace, L.sums)};
+                at<uint64_t>(workspace, L.sums), L.count_cap};
   const dim3 grid((unsigned)cdiv(n, kBlock));
   LAUNCH_N("tag_pack", n, k_pack, grid, dim3(kBlock), s, *in, recs);
   int field_bits = 0;
@@ -928,7 +939,7 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
     if (h[0] > 0) {  // runs longer than kTieShort: (run, tiebreak) radix sort of their records
       const int tie_bits = bitlen((uint64_t)n_tiebreak_ids);
       SortBuffers LB{at<uint64_t>(workspace, L.lka), at<uint64_t>(workspace, L.lkb), at<uint32_t>(workspace, L.lva),
-                     at<uint32_t>(workspace, L.lvb), B.counts, B.offsets, B.sums};
+                     at<uint32_t>(workspace, L.lvb), B.counts, B.offsets, B.sums, B.count_cap};
       LAUNCH("tag_long_keys", k_long_keys, dim3(h[0]), dim3(kBlock), s, (const uint4*)longs, (const uint32_t*)perm,
              tiebreak, tie_bits, LB.ka, LB.va, pos_of);
       int w2 = 0;
@@ -1029,7 +1040,7 @@ int sct_count_matrix(const sct_count_input_t* in, sct_count_output_t* out, void*
   const int64_t nc = in->n_cell_ids;
   SortBuffers B{at<uint64_t>(workspace, L.ka), at<uint64_t>(workspace, L.kb), at<uint32_t>(workspace, L.va),
                 at<uint32_t>(workspace, L.vb), at<uint32_t>(workspace, L.counts), at<uint32_t>(workspace, L.offsets),
-                at<uint64_t>(workspace, L.sums)};
+                at<uint64_t>(workspace, L.sums), L.count_cap};
   uint32_t* fa = at<uint32_t>(workspace, L.flags_a);
   uint32_t* oa = at<uint32_t>(workspace, L.offs_a);
   uint32_t* fb = at<uint32_t>(workspace, L.flags_b);

@@ -74,11 +74,14 @@ class _Handle:
         import torch
 
         self.L = load()
-        self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if dev.index is None:  # "cuda": the current device, for the library and the stream alike
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.dev = dev
         self.stream = torch.cuda.current_stream(self.dev)
         self.h = ctypes.c_void_p()
         n = ctypes.c_int64(0)
-        self.rc = self.L.sct_gbam_open(os.fsencode(path), int(self.dev.index or 0),
+        self.rc = self.L.sct_gbam_open(os.fsencode(path), int(self.dev.index),
                                        ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h), ctypes.byref(n))
         self.n = int(n.value)
 
@@ -119,16 +122,21 @@ def decode(path: str, metric_mode: str = "cell", device=None, timings: Optional[
         _check(H.rc)
         if H.rc == HOST:
             return None
+        if metric_mode == "count" and (tags is None or len(tags) != 3 or any(len(t) != 2 for t in tags)):
+            raise ValueError("count mode needs three 2-character tag names")
+        names_ = COUNT_COLUMNS if metric_mode == "count" else N.RECORD_COLUMNS
+        try:  # columns that do not fit the device: the host decoder takes the file
+            if metric_mode == "count":
+                cols = {c: torch.empty(H.n, dtype=torch.int32 if c in ("cell", "umi", "gene") else torch.uint8,
+                                       device=H.dev) for c in COUNT_COLUMNS}
+            else:
+                cols = {c: torch.empty(H.n, dtype=_TORCH_DTYPES[c], device=H.dev) for c in N.RECORD_COLUMNS}
+        except torch.cuda.OutOfMemoryError:
+            return None
+        ptrs = (ctypes.c_void_p * len(names_))(*[cols[c].data_ptr() for c in names_])
         if metric_mode == "count":
-            if tags is None or len(tags) != 3 or any(len(t) != 2 for t in tags):
-                raise ValueError("count mode needs three 2-character tag names")
-            cols = {c: torch.empty(H.n, dtype=torch.int32 if c in ("cell", "umi", "gene") else torch.uint8,
-                                   device=H.dev) for c in COUNT_COLUMNS}
-            ptrs = (ctypes.c_void_p * len(COUNT_COLUMNS))(*[cols[c].data_ptr() for c in COUNT_COLUMNS])
             rc = H.L.sct_gbam_parse_count(H.h, "".join(tags).encode("ascii"), ptrs)
         else:
-            cols = {c: torch.empty(H.n, dtype=_TORCH_DTYPES[c], device=H.dev) for c in N.RECORD_COLUMNS}
-            ptrs = (ctypes.c_void_p * len(N.RECORD_COLUMNS))(*[cols[c].data_ptr() for c in N.RECORD_COLUMNS])
             rc = H.L.sct_gbam_parse(H.h, _MODES[metric_mode], ptrs)
         _check(rc)
         if rc == HOST:

@@ -19,6 +19,16 @@ the distinct counts and the Welford mean / variance, and fills every public
 attribute from the engine's row.  ``finalize`` of an aggregator that parsed
 nothing gives the reference's values (zero counts, 0.0 means, NaN variances
 and ratios) without a launch.
+
+Known gap: a record that raises part-way (``KeyError`` on XF or NH
+of a mapped read, ``ZeroDivisionError`` / ``TypeError`` on its qualities) is
+not buffered.  The reference has by then already fed that record to its
+molecule histogram and its UY / genomic Welford streams (and, for XF / NH, its
+fragment histogram), so a caller that *catches* the error and still calls
+``finalize()`` gets n_molecules, n_fragments and the stream means of the
+records before it only.  The gatherers never do that (the error aborts
+``extract_metrics``, as in the reference), and the integer counters the
+reference updates before the raise point are kept exactly.
 """
 
 from typing import Sequence

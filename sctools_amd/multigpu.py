@@ -161,6 +161,7 @@ class DeviceGroup:
                         for d in self.devices]
         self.lib = N.load()
         self._comms: Optional[ctypes.Array] = None
+        self._aborted = False  # communicators aborted: never re-created (a late rank would hang on them)
         self._run: Optional[GroupRun] = None
         self._slots: List[Optional[torch.Tensor]] = [None] * len(self.devices)
 
@@ -182,12 +183,24 @@ class DeviceGroup:
         on the caller's thread before the ranks' threads use them."""
         if self.shared:
             return None
+        if self._aborted:
+            raise GroupAborted("the group's communicators were aborted after a rank failed")
         if self._comms is None:
             comms = (ctypes.c_void_p * self.size)()
             devs = (ctypes.c_int * self.size)(*self.devices)
             N.check(self.lib.sct_comm_init_all(comms, self.size, devs))
             self._comms = comms
         return self._comms
+
+    def _rank_comm(self, rank: int) -> int:
+        """A rank thread's communicator: created beforehand on the caller's thread (comms()); never
+        created here, so a rank that arrives after an abort raises instead of re-initialising."""
+        comms = self._comms
+        if comms is None:
+            if self._aborted:
+                raise GroupAborted("the group's communicators were aborted after a rank failed")
+            raise RuntimeError("DeviceGroup.comms() must be called before the ranks run")
+        return comms[rank]
 
     def allreduce_partials(self, rank: int, partials: torch.Tensor) -> None:
         """In-place sum of every rank's [rows, SCT_NP] int64 partials (call from every rank's thread,
@@ -203,7 +216,7 @@ class DeviceGroup:
             self._local_sum(rank, partials)
             return
         N.check(self.lib.sct_allreduce_gene_partials(ctypes.c_void_p(partials.data_ptr()), int(partials.shape[0]),
-                                                     ctypes.c_void_p(self.comms()[rank]),
+                                                     ctypes.c_void_p(self._rank_comm(rank)),
                                                      ctypes.c_void_p(stream.cuda_stream)))
         done = torch.cuda.Event()
         done.record(stream)
@@ -229,7 +242,10 @@ class DeviceGroup:
             self._slots = [None] * self.size
 
     def abort(self) -> None:
-        """A rank failed: cancel the collective on every communicator (ncclCommAbort)."""
+        """A rank failed: cancel the collective on every communicator (ncclCommAbort).  The group
+        stays aborted: a rank that reaches comms() afterwards raises GroupAborted instead of
+        initialising fresh communicators whose peers never come."""
+        self._aborted = True
         if self._comms is not None:
             comms, self._comms = self._comms, None
             for c in comms:

@@ -182,3 +182,22 @@ def test_repeated_records_converge(tmp_path):
     assert tm["start_rounds"] < 64
     same_as_host(path, "gene")
     same_as_host(path, "cell")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [1, 200_000])
+def test_device_memory_exhausted_declines(tmp_path, monkeypatch, cap):
+    """A device allocation that fails (here: past SCT_GBAM_MAX_DEVICE_BYTES, as hipMalloc fails when
+    HBM is exhausted) declines the file instead of raising: ``decode`` returns None and
+    the gatherer's CSV, made by the host decoder, is still the reference's."""
+    from sctools_amd.metrics import GatherCellMetrics
+
+    path = os.path.join(GOLD, "cell-sorted-missing-cb.bam")
+    monkeypatch.setenv("SCT_GBAM_MAX_DEVICE_BYTES", str(cap))
+    assert gbam.decode(path, "cell") is None
+    assert "device memory" in gbam.last_error()
+    stem = str(tmp_path / "out")
+    GatherCellMetrics(path, stem, compress=False).extract_metrics()
+    assert open(stem + ".csv").read() == H.golden_text("cell-sorted-missing-cb", "cell")
+    monkeypatch.delenv("SCT_GBAM_MAX_DEVICE_BYTES")
+    same_as_host(path, "cell")  # the cap gone, the device decodes it again

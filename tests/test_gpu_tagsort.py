@@ -145,6 +145,44 @@ def test_tag_sort_with_keys_wider_than_64_bits(eng):
 
 
 @pytest.mark.gpu
+def test_tag_sort_small_radix_tiles():
+    """The engine built with 1024-item radix tiles (tests/native/libsct_engine_si4.so) sorts like
+    numpy.  Round 3's tag-sort layout sized the digit counts by the 2048-record row tile, so this
+    tiling overflowed them (an illegal memory access in config 5's sort); the counts
+    now cover both tilings and radix_sort checks its capacity.  Runs in a child process (one
+    engine library per process)."""
+    import subprocess
+    import sys
+
+    lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "libsct_engine_si4.so")
+    assert os.path.exists(lib), "build it first: make tests/native/libsct_engine_si4.so"
+    env = dict(os.environ, SCT_LIB_PATH=lib)
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(lib), "..", "si4_check.py"), "2000000"], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.count("equal numpy's lexsort") == 2, r.stdout
+
+
+def test_tag_sort_workspace_covers_every_radix_tiling():
+    """CPU: the tag-sort workspace holds the digit counts of radix_sort's tiles (kSortTile), not
+    only the row passes' (kRowTile).  The si4 engine (1024-item tiles) needs 256 counts per 1024
+    records in each of `counts` and `offsets` on top of the 56 B/record of rows and key buffers."""
+    import ctypes
+
+    lib_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "libsct_engine_si4.so")
+    if not os.path.exists(lib_path):
+        pytest.skip("tests/native/libsct_engine_si4.so not built")
+    lib = ctypes.CDLL(lib_path)
+    n = 1 << 20
+    plan = N.Plan(n_records=n, n_cell_ids=1, n_gene_ids=1, n_umi_ids=1)
+    a, b = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    assert N.load().sct_tag_sort_workspace_size(ctypes.byref(plan), ctypes.byref(a)) == 0
+    assert lib.sct_tag_sort_workspace_size(ctypes.byref(plan), ctypes.byref(b)) == 0
+    # 2 x 4 B x 256 counts per tile: the si4 build has twice the tiles of the shipped one
+    assert b.value - a.value >= 2 * 4 * 256 * (n // 1024 - n // 2048)
+
+
+@pytest.mark.gpu
 def test_verify_sort_finds_the_first_violation(eng):
     from sctools_amd import engine as E
 

@@ -7,6 +7,7 @@ whose peers never come; a rank that fails while a collective is in flight must c
 barrier, which blocks exactly as an all-reduce with a missing peer does.
 """
 
+import ctypes
 import threading
 import time
 
@@ -144,3 +145,35 @@ def test_parse_devices_allows_shards_sharing_a_device():
         parse_devices(0)
     with pytest.raises(ValueError):
         parse_devices([])
+
+
+def test_device_group_stays_aborted():
+    """after abort() a rank reaching its communicator raises GroupAborted; neither it nor
+    comms() re-initialises communicators (a fresh ncclCommInitAll from a late rank would issue an
+    all-reduce whose peers never come).  CPU: a DeviceGroup shell with a stub library."""
+    from sctools_amd.multigpu import DeviceGroup
+
+    class Lib:
+        def __init__(self):
+            self.aborted, self.inits = [], 0
+
+        def sct_comm_abort(self, c):
+            self.aborted.append(c.value)
+
+        def sct_comm_init_all(self, *a):
+            self.inits += 1
+            return 0
+
+    g = object.__new__(DeviceGroup)
+    g.devices, g.shared, g.lib, g._run, g._aborted = [0, 1], False, Lib(), None, False
+    g._comms = (ctypes.c_void_p * 2)(11, 12)
+    assert g._rank_comm(1) == 12
+    g.abort()
+    assert g.lib.aborted == [11, 12]
+    with pytest.raises(GroupAborted):
+        g._rank_comm(0)
+    with pytest.raises(GroupAborted):
+        g.comms()
+    assert g.lib.inits == 0
+    g.abort()  # idempotent: nothing left to abort
+    assert g.lib.aborted == [11, 12]
