@@ -37,6 +37,31 @@ typedef struct sct_gbam sct_gbam_t;
  * SCT_BAM_E* code (sct_bam.h) otherwise, with *out NULL. */
 int sct_gbam_open(const char* path, int32_t device, void* stream, sct_gbam_t** out, int64_t* n_records);
 
+/* Phase 1 for one of `n_parts` devices decoding one file together (GatherCellMetrics(devices=N)):
+ * part `part` takes the BGZF members from the first one starting at or after part/n_parts of the
+ * file's bytes to the next part's first (byte-balanced; part 0 keeps the header's) and the records
+ * starting in their payload; a record cut by the part's end is read on from the next part's
+ * members.  first_start: the payload offset of the part's first record, or -1 to find it inside the
+ * part (then check it: sct_gbam_part_bounds).  A part may hold no records (*n_records 0: skip its
+ * parse).  Same returns as sct_gbam_open. */
+int sct_gbam_open_part(const char* path, int32_t part, int32_t n_parts, int64_t first_start, int32_t device,
+                       void* stream, sct_gbam_t** out, int64_t* n_records);
+
+/* Payload offsets of a part's first record and of the first record after the part (its walk's
+ * landing).  Part p's first_start must equal part p-1's end_landing; if not, reopen part p with
+ * first_start = part p-1's end_landing (the walk from inside part p guessed wrong). */
+int sct_gbam_part_bounds(const sct_gbam_t* h, int64_t* first_start, int64_t* end_landing);
+
+/* After every part's parse: the parts' dictionaries `which` merged into one ranked dictionary (the
+ * sorted union, the missing tag first if any part has it; sct_gbam_dictionary(parts[0], which)
+ * returns it) and remap[p][i] = the merged id of part p's id i (caller-sized host arrays, one entry
+ * per id of part p's dictionary).  Then sct_gbam_remap renumbers each part's column. */
+int sct_gbam_merge_dictionaries(sct_gbam_t* const* parts, int32_t n_parts, int32_t which, int32_t* const* remap);
+
+/* column[i] = remap[column[i]] for the n int32 ids of a device column, on the part's device and
+ * stream (remap: n_ids host entries). */
+int sct_gbam_remap(sct_gbam_t* h, const int32_t* remap, int64_t n_ids, void* column, int64_t n);
+
 /* Phase 2: parse the records into the caller's device columns, in the order of
  * sct_records_t (include/sctools_gpu.h): cell, umi, gene, ref, pos (int32), gq_sum, gq_len,
  * gq_gt30 (uint16), bits, xf, cy_gt30, cy_len, uy_gt30, uy_len (uint8); each holds
@@ -68,6 +93,14 @@ int sct_gbam_read_inflated(const sct_gbam_t* h, uint64_t off, uint64_t n, void* 
  * inflating while the next piece copies), [2] the inflate left after the last piece, [3] record
  * starts, [4] parse + intern, [5] dictionaries, [6] members, [7] record-start repair rounds. */
 int sct_gbam_timing(const sct_gbam_t* h, double* t8);
+
+/* Decode windows of the file (1: the whole payload was resident at once).  A BAM whose payload
+ * exceeds SCT_GBAM_WINDOW_BYTES (default: a quarter of the device's free memory) is decoded in
+ * windows of whole BGZF members, twice inflated: sct_gbam_open proves record starts and counts
+ * records window by window, sct_gbam_parse re-inflates and parses them, so device memory holds one
+ * window's payload, the columns and the dictionaries (the reference reads in bounded memory too:
+ * bam.py:361-488 splits, htslib_tagsort.cpp:308-393 streams). */
+int64_t sct_gbam_windows(const sct_gbam_t* h);
 
 /* Free the device buffers. */
 void sct_gbam_close(sct_gbam_t* h);

@@ -173,6 +173,108 @@ class Columns:
         return mito, multi
 
 
+class ShardedColumns:
+    """Device columns of one file held as contiguous record ranges on several devices (``gbam``'s
+    per-device decode, ``GatherCellMetrics(devices=N)``): shard r holds records
+    ``offsets[r] .. offsets[r + 1]`` of the file, in file order, on its device; the dictionaries
+    are global.  Shards are cut at runs of ``key`` (cut_runs), so an entity never spans two."""
+
+    on_device = True
+
+    def __init__(self, shards: List[Dict], cells, umis, genes):
+        self.shards = shards
+        self.cells = cells
+        self.umis = umis
+        self.genes = genes
+
+    @property
+    def offsets(self) -> List[int]:
+        out = [0]
+        for sh in self.shards:
+            out.append(out[-1] + int(sh["cell"].shape[0]))
+        return out
+
+    @property
+    def n(self) -> int:
+        return self.offsets[-1]
+
+    def host(self) -> "Columns":
+        """One host Columns of every shard's records, in order (tests)."""
+        arrays = {}
+        for c in self.shards[0]:
+            parts = [sh[c].cpu().numpy() for sh in self.shards]
+            a = np.concatenate(parts)
+            arrays[c] = a.view(np.uint16) if a.dtype == np.int16 else a
+        return Columns(arrays, self.cells, self.umis, self.genes)
+
+    def column_at(self, name: str, index: np.ndarray) -> np.ndarray:
+        """Column ``name`` at file-wide record indices, gathered on the shards' devices."""
+        import torch
+
+        index = np.asarray(index, dtype=np.int64)
+        off = np.asarray(self.offsets, dtype=np.int64)
+        which = np.searchsorted(off, index, side="right") - 1
+        out = None
+        for r, sh in enumerate(self.shards):
+            sel = np.flatnonzero(which == r)
+            if not sel.size:
+                continue
+            t = sh[name]
+            idx = torch.from_numpy(index[sel] - off[r]).to(t.device)
+            v = t[idx].cpu().numpy()
+            if out is None:
+                out = np.empty(index.shape[0], dtype=v.dtype)
+            out[sel] = v
+        if out is None:
+            out = np.empty(0, dtype=np.int32)
+        return out
+
+    gene_flags = Columns.gene_flags
+
+
+def cut_runs(shards: List[Dict], key: str) -> List[Dict]:
+    """Shards re-cut so that no run of equal ``key`` values spans two: the records at the head of a
+    shard continuing the previous (non-empty) shard's last run move to the end of that shard --
+    SplitBam's invariant (bam.py:439-448), an entity's records on one device.  Columns moved or
+    left behind are fresh 16-byte-aligned buffers (the kernels' vector loads need them)."""
+    import torch
+
+    shards = [dict(sh) for sh in shards]
+    prev = None
+    for r in range(len(shards)):
+        sh = shards[r]
+        n = int(sh[key].shape[0])
+        if n == 0:
+            continue
+        if prev is not None:
+            last = shards[prev][key][-1]
+            col = sh[key]
+            if bool((col[0] == last).item()):
+                diff = torch.nonzero(col != col[0])
+                k = int(diff[0, 0].item()) if diff.numel() else n
+                dst = shards[prev][key].device
+                for c in list(sh.keys()):
+                    moved = sh[c][:k].to(dst)
+                    shards[prev][c] = torch.cat((shards[prev][c], moved))
+                    sh[c] = sh[c][k:].clone()
+                if k == n:
+                    continue  # the whole shard continued the run: the next one compares with prev
+        prev = r
+    return shards
+
+
+def columnarize_parts(path: str, metric_mode: str, devices, key: str) -> Optional[ShardedColumns]:
+    """A BAM decoded by ``devices`` together (``gbam.decode_parts``: part r on devices[r]), shards
+    cut at runs of ``key``; None when the file needs the host decoder."""
+    from sctools_amd import gbam
+
+    got = gbam.decode_parts(path, metric_mode, devices)
+    if got is None:
+        return None
+    shards, (cn, un, gn) = got
+    return ShardedColumns(cut_runs(shards, key), cn, un, gn)
+
+
 def _frac_counts(quality_string: str):
     # _quality_string_to_numeric + _quality_above_threshold (aggregator.py:191-231)
     n = len(quality_string)

@@ -24,8 +24,9 @@ LIB_PATH = os.environ.get("SCT_GBAM_LIB_PATH") or os.path.join(HERE, "libsct_gba
 
 OK, HOST = 0, 1
 _MODES = {"cell": 0, "gene": 1}
-EXPORTED = ("sct_gbam_open", "sct_gbam_parse", "sct_gbam_parse_count", "sct_gbam_dictionary", "sct_gbam_read_inflated", "sct_gbam_timing",
-            "sct_gbam_close", "sct_gbam_last_error")
+EXPORTED = ("sct_gbam_open", "sct_gbam_open_part", "sct_gbam_part_bounds", "sct_gbam_merge_dictionaries",
+            "sct_gbam_remap", "sct_gbam_parse", "sct_gbam_parse_count", "sct_gbam_dictionary", "sct_gbam_read_inflated",
+            "sct_gbam_timing", "sct_gbam_windows", "sct_gbam_close", "sct_gbam_last_error")
 STAGES = ("map_scan", "h2d", "inflate", "record_starts", "parse_intern", "dictionaries", "members",
           "start_rounds")
 
@@ -46,6 +47,14 @@ def load() -> ctypes.CDLL:
     vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
     L.sct_gbam_open.restype = ctypes.c_int
     L.sct_gbam_open.argtypes = [ctypes.c_char_p, i32, vp, ctypes.POINTER(vp), ctypes.POINTER(i64)]
+    L.sct_gbam_open_part.restype = ctypes.c_int
+    L.sct_gbam_open_part.argtypes = [ctypes.c_char_p, i32, i32, i64, i32, vp, ctypes.POINTER(vp), ctypes.POINTER(i64)]
+    L.sct_gbam_part_bounds.restype = ctypes.c_int
+    L.sct_gbam_part_bounds.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+    L.sct_gbam_merge_dictionaries.restype = ctypes.c_int
+    L.sct_gbam_merge_dictionaries.argtypes = [ctypes.POINTER(vp), i32, i32, ctypes.POINTER(ctypes.POINTER(i32))]
+    L.sct_gbam_remap.restype = ctypes.c_int
+    L.sct_gbam_remap.argtypes = [vp, ctypes.POINTER(i32), i64, vp, i64]
     L.sct_gbam_parse.restype = ctypes.c_int
     L.sct_gbam_parse.argtypes = [vp, i32, ctypes.POINTER(vp)]
     L.sct_gbam_parse_count.restype = ctypes.c_int
@@ -57,6 +66,8 @@ def load() -> ctypes.CDLL:
     L.sct_gbam_read_inflated.argtypes = [vp, u64, u64, vp, ctypes.POINTER(u64)]
     L.sct_gbam_timing.restype = ctypes.c_int
     L.sct_gbam_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+    L.sct_gbam_windows.restype = ctypes.c_int64
+    L.sct_gbam_windows.argtypes = [vp]
     L.sct_gbam_close.restype = None
     L.sct_gbam_close.argtypes = [vp]
     L.sct_gbam_last_error.restype = ctypes.c_char_p
@@ -69,21 +80,53 @@ def last_error() -> str:
     return load().sct_gbam_last_error().decode("utf-8", "replace")
 
 
+def _device(device):
+    import torch
+
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if dev.index is None:  # "cuda": the current device, for the library and the stream alike
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
 class _Handle:
-    def __init__(self, path: str, device):
+    def __init__(self, path: str, device, part: int = 0, n_parts: int = 1, first_start: int = -1):
         import torch
 
         self.L = load()
-        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        if dev.index is None:  # "cuda": the current device, for the library and the stream alike
-            dev = torch.device("cuda", torch.cuda.current_device())
-        self.dev = dev
+        self.dev = _device(device)
         self.stream = torch.cuda.current_stream(self.dev)
         self.h = ctypes.c_void_p()
         n = ctypes.c_int64(0)
-        self.rc = self.L.sct_gbam_open(os.fsencode(path), int(self.dev.index),
-                                       ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h), ctypes.byref(n))
+        self.rc = self.L.sct_gbam_open_part(os.fsencode(path), int(part), int(n_parts), int(first_start),
+                                            int(self.dev.index), ctypes.c_void_p(self.stream.cuda_stream),
+                                            ctypes.byref(self.h), ctypes.byref(n))
         self.n = int(n.value)
+
+    def bounds(self):
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        _check(self.L.sct_gbam_part_bounds(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return int(a.value), int(b.value)
+
+    def dictionary(self, which: int, lazy: bool = True):
+        cnt, by, off, hn = ctypes.c_int64(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int32()
+        self.L.sct_gbam_dictionary(self.h, which, ctypes.byref(cnt), ctypes.byref(by), ctypes.byref(off),
+                                   ctypes.byref(hn))
+        k = int(cnt.value)
+        if k == 0 or not off.value:
+            offs = np.zeros(1, dtype=np.int64)
+        else:
+            offs = np.frombuffer((ctypes.c_int64 * (k + 1)).from_address(off.value), dtype=np.int64).copy()
+        total = int(offs[-1])
+        raw = ctypes.string_at(by.value, total) if total else b""
+        if lazy:
+            from sctools_amd.columnar import PackedDictionary
+
+            return PackedDictionary(raw, offs, bool(hn.value))
+        lst = [raw[offs[i]:offs[i + 1]].decode("utf-8") for i in range(k)]
+        if hn.value:
+            lst[0] = None
+        return lst
 
     def close(self):
         if self.h:
@@ -93,7 +136,9 @@ class _Handle:
     def timing(self):
         t = (ctypes.c_double * 8)()
         self.L.sct_gbam_timing(self.h, t)
-        return dict(zip(STAGES, list(t)))
+        out = dict(zip(STAGES, list(t)))
+        out["windows"] = int(self.L.sct_gbam_windows(self.h))
+        return out
 
 
 def _check(rc: int):
@@ -141,24 +186,7 @@ def decode(path: str, metric_mode: str = "cell", device=None, timings: Optional[
         _check(rc)
         if rc == HOST:
             return None
-        names = []
-        for which in range(3):
-            cnt, by, off, hn = ctypes.c_int64(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int32()
-            H.L.sct_gbam_dictionary(H.h, which, ctypes.byref(cnt), ctypes.byref(by), ctypes.byref(off),
-                                    ctypes.byref(hn))
-            k = int(cnt.value)
-            offs = np.frombuffer((ctypes.c_int64 * (k + 1)).from_address(off.value), dtype=np.int64).copy()
-            total = int(offs[-1])
-            raw = ctypes.string_at(by.value, total) if total else b""
-            if lazy:
-                from sctools_amd.columnar import PackedDictionary
-
-                names.append(PackedDictionary(raw, offs, bool(hn.value)))
-                continue
-            lst = [raw[offs[i]:offs[i + 1]].decode("utf-8") for i in range(k)]
-            if hn.value:
-                lst[0] = None
-            names.append(lst)
+        names = [H.dictionary(which, lazy) for which in range(3)]
         if timings is not None:
             timings.update(H.timing())
         return cols, names
@@ -182,3 +210,113 @@ def inflate(path: str, device=None) -> Optional[bytes]:
         return buf.raw
     finally:
         H.close()
+
+
+def decode_parts(path: str, metric_mode: str, devices, timings: Optional[dict] = None):
+    """One file decoded by several devices together (``GatherCellMetrics(devices=N)``): part p of
+    len(devices) -- a byte-balanced range of BGZF members and the records starting in them -- is
+    inflated, parsed and interned on devices[p] (``sct_gbam_open_part``), so no device holds the
+    whole file.  The parts' record starts are checked against each other (part p's first record is
+    the landing of part p-1's walk; a part that guessed wrong is reopened there), their dictionaries
+    merged into the global ranked ones and every part's ids renumbered on its device.
+
+    Returns (per-part column dicts on their devices, [cells, umis, genes] ``PackedDictionary``) --
+    records in file order, part after part -- or None when the file needs the host decoder."""
+    import threading
+
+    import torch
+
+    from sctools_amd import _native as N
+    from sctools_amd.engine import _TORCH_DTYPES
+
+    if metric_mode not in _MODES:
+        raise ValueError("decode_parts reads the cell and gene metric modes")
+    devs = [_device(d) for d in devices]
+    P = len(devs)
+    hs: list = [None] * P
+    errs: list = [None] * P
+
+    def each(fn):
+        def work(p):
+            try:
+                with torch.cuda.device(devs[p]):
+                    fn(p)
+            except BaseException as e:  # noqa: BLE001 -- re-raised below
+                errs[p] = e
+
+        th = [threading.Thread(target=work, args=(p,)) for p in range(P)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for e in errs:
+            if e is not None:
+                raise e
+
+    def close_all():
+        for h in hs:
+            if h is not None:
+                h.close()
+
+    try:
+        def open_one(p):
+            hs[p] = _Handle(path, devs[p], p, P)
+
+        each(open_one)
+        for h in hs:
+            _check(h.rc)
+        if any(h.rc == HOST for h in hs):
+            return None
+        for p in range(1, P):  # part p starts where part p-1's walk lands
+            land = hs[p - 1].bounds()[1]
+            if hs[p].bounds()[0] != land:
+                hs[p].close()
+                with torch.cuda.device(devs[p]):
+                    hs[p] = _Handle(path, devs[p], p, P, first_start=land)
+                _check(hs[p].rc)
+                if hs[p].rc == HOST:
+                    return None
+        cols: list = [None] * P
+        rcs = [OK] * P
+
+        def parse_one(p):
+            h = hs[p]
+            cols[p] = {c: torch.empty(h.n, dtype=_TORCH_DTYPES[c], device=h.dev) for c in N.RECORD_COLUMNS}
+            if h.n:
+                ptrs = (ctypes.c_void_p * len(N.RECORD_COLUMNS))(*[cols[p][c].data_ptr() for c in N.RECORD_COLUMNS])
+                rcs[p] = h.L.sct_gbam_parse(h.h, _MODES[metric_mode], ptrs)
+
+        each(parse_one)
+        for rc in rcs:
+            _check(rc)
+        if any(rc == HOST for rc in rcs):
+            return None
+        L = load()
+        remaps = []
+        for which in range(3):
+            sizes = [len(hs[p].dictionary(which)) for p in range(P)]
+            arrs = [np.zeros(max(1, k), dtype=np.int32) for k in sizes]
+            ptrs = (ctypes.POINTER(ctypes.c_int32) * P)(
+                *[a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)) for a in arrs])
+            handles = (ctypes.c_void_p * P)(*[h.h.value for h in hs])
+            _check(L.sct_gbam_merge_dictionaries(handles, P, which, ptrs))
+            remaps.append((arrs, sizes))
+
+        def remap_one(p):
+            h = hs[p]
+            if not h.n:
+                return
+            for which, col in enumerate(("cell", "umi", "gene")):
+                arrs, sizes = remaps[which]
+                a = arrs[p]
+                _check(h.L.sct_gbam_remap(h.h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), sizes[p],
+                                          ctypes.c_void_p(cols[p][col].data_ptr()), h.n))
+
+        each(remap_one)
+        names = [hs[0].dictionary(which) for which in range(3)]
+        if timings is not None:
+            timings.update(hs[0].timing())
+            timings["parts"] = [h.n for h in hs]
+        return cols, names
+    finally:
+        close_all()

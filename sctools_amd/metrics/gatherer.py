@@ -96,11 +96,18 @@ class MetricGatherer:
             if gbam.available():
                 if self._devices is None:
                     dev = E.get_engine(self._device).device
-                else:  # several devices: decode on the first, the shards are copied device to device
-                    from sctools_amd import multigpu
+                    return columnar.columnarize(self.bam_file, mode, metric_mode, device=dev)
+                # several devices: each decodes its part of the file (no device holds it all), the
+                # parts re-cut at entity runs; a file the device path declines: the host decoder
+                import torch
 
-                    dev = E.get_engine(multigpu.parse_devices(self._devices)[0]).device
-                return columnar.columnarize(self.bam_file, mode, metric_mode, device=dev)
+                from sctools_amd import multigpu
+
+                devs = [torch.device("cuda", d) for d in multigpu.parse_devices(self._devices)]
+                key = "cell" if metric_mode == columnar.MODE_CELL else "gene"
+                got = columnar.columnarize_parts(self.bam_file, metric_mode, devs, key)
+                if got is not None:
+                    return got
         return columnar.columnarize(self.bam_file, mode, metric_mode)
 
     @property

@@ -264,6 +264,52 @@ class DeviceGroup:
         self.close()
 
 
+def _bounds(cols, key, size: int):
+    """Each rank's record range [lo, hi): the decoded shards as they are (ShardedColumns), or
+    run-aligned, record-balanced cuts of one column set."""
+    if isinstance(cols, columnar.ShardedColumns):
+        off = cols.offsets
+        if len(off) - 1 != size:
+            raise ValueError("%d decoded shards for %d devices" % (len(off) - 1, size))
+        return [(off[r], off[r + 1]) for r in range(size)]
+    return D.shard_bounds(cols.arrays[key], size)
+
+
+def _rank_cols(cols, r: int, lo: int, hi: int, device) -> dict:
+    """Rank r's columns on its device: its decoded shard, or records [lo, hi) copied there."""
+    if isinstance(cols, columnar.ShardedColumns):
+        sh = cols.shards[r]
+        if sh["cell"].device != device:
+            sh = {c: t.to(device) for c, t in sh.items()}
+        return sh
+    return _shard_to(cols, lo, hi, device)
+
+
+def _cells_twice(cols) -> bool:
+    """A cell barcode forming two runs (the records are not cell-sorted)."""
+    if isinstance(cols, columnar.ShardedColumns):
+        hv = []
+        for sh in cols.shards:
+            c = sh["cell"]
+            if c.shape[0]:
+                hv.append(c[torch.cat((torch.zeros(1, dtype=torch.long, device=c.device),
+                                       torch.nonzero(c[1:] != c[:-1]).flatten() + 1))].cpu().numpy())
+        if not hv:
+            return False
+        heads = np.concatenate(hv)
+        keep = np.concatenate(([True], heads[1:] != heads[:-1]))  # (shards are cut at runs)
+        return np.bincount(heads[keep]).max() > 1
+    cell = cols.arrays["cell"]
+    if not cell.shape[0]:
+        return False
+    if cols.on_device:
+        heads = cell[torch.cat((torch.zeros(1, dtype=torch.long, device=cell.device),
+                                torch.nonzero(cell[1:] != cell[:-1]).flatten() + 1))]
+        return int(torch.bincount(heads.long()).max().item()) > 1
+    heads = cell[np.concatenate(([0], np.flatnonzero(cell[1:] != cell[:-1]) + 1))]
+    return np.bincount(heads).max() > 1
+
+
 def _shard_to(cols: columnar.Columns, lo: int, hi: int, device) -> dict:
     """Records [lo, hi) of every column on ``device``: host columns are copied up; device columns
     (decoded on the GPU, ``gbam``) are sliced in place and copied device to device (over xGMI when
@@ -287,18 +333,18 @@ def compute_rows(cols: columnar.Columns, mode: str, mitochondrial_gene_ids=froze
     same order, as one device computes (``metrics.gatherer.compute_rows``)."""
     from sctools_amd import engine as E
 
-    key = cols.arrays["cell" if mode == "cell" else "gene"]
+    key = "cell" if mode == "cell" else "gene"
     mito, multi = cols.gene_flags(mitochondrial_gene_ids)
     dims = _dims(cols)
     with DeviceGroup(devices) as g:
-        bounds = D.shard_bounds(key, g.size)
+        bounds = _bounds(cols, key, g.size)
 
         def rank_rows(r):
             lo, hi = bounds[r]
             if hi == lo:
                 return np.zeros((0, N.SCT_NI), np.int64), np.zeros((0, N.SCT_NF), np.float64)
             eng = g.engines[r]
-            dev_cols = _shard_to(cols, lo, hi, eng.device)
+            dev_cols = _rank_cols(cols, r, lo, hi, eng.device)
             gm = torch.from_numpy(mito).to(eng.device)
             gx = torch.from_numpy(multi).to(eng.device)
             ints, floats = eng.compute(dev_cols, mode, dims, gm, gx, float_mode=float_mode)
@@ -318,27 +364,19 @@ def compute_cell_and_gene_rows(cols: columnar.Columns, mitochondrial_gene_ids=fr
     gene rows are indexed by gene id (zero-read ids included; the writer skips them)."""
     from sctools_amd import engine as E
 
-    cell = cols.arrays["cell"]
-    if cell.shape[0]:  # grouped gene rows need every cell in ONE run (the cell-sharding invariant)
-        if cols.on_device:
-            heads = cell[torch.cat((torch.zeros(1, dtype=torch.long, device=cell.device),
-                                    torch.nonzero(cell[1:] != cell[:-1]).flatten() + 1))]
-            twice = int(torch.bincount(heads.long()).max().item()) > 1
-        else:
-            heads = cell[np.concatenate(([0], np.flatnonzero(cell[1:] != cell[:-1]) + 1))]
-            twice = np.bincount(heads).max() > 1
-        if twice:
-            raise ValueError("gene rows of a record set need cell-sorted records (a cell barcode forms two runs)")
+    # grouped gene rows need every cell in ONE run (the cell-sharding invariant)
+    if _cells_twice(cols):
+        raise ValueError("gene rows of a record set need cell-sorted records (a cell barcode forms two runs)")
     mito, multi = cols.gene_flags(mitochondrial_gene_ids)
     dims = _dims(cols)
     with DeviceGroup(devices) as g:
-        bounds = D.shard_bounds(cell, g.size)
+        bounds = _bounds(cols, "cell", g.size)
         g.comms()
 
         def rank_rows(r):
             lo, hi = bounds[r]
             eng = g.engines[r]
-            dev_cols = _shard_to(cols, lo, hi, eng.device)
+            dev_cols = _rank_cols(cols, r, lo, hi, eng.device)
             gm = torch.from_numpy(mito).to(eng.device)
             gx = torch.from_numpy(multi).to(eng.device)
             if hi == lo:

@@ -25,7 +25,7 @@ BAMS = sorted(f[:-4] for f in os.listdir(GOLD) if f.endswith(".bam"))
 
 def test_every_declared_symbol_is_exported():
     text = open(os.path.join(ROOT, "include", "sct_gbam.h")).read()
-    names = sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(sct_\w+)\(", text, flags=re.M)))
+    names = sorted(set(re.findall(r"^\s*(?:int|int64_t|void|const char\*)\s+(sct_\w+)\(", text, flags=re.M)))
     assert set(names) == set(gbam.EXPORTED)
     lib = gbam.load()
     for name in names:
@@ -201,3 +201,101 @@ def test_device_memory_exhausted_declines(tmp_path, monkeypatch, cap):
     assert open(stem + ".csv").read() == H.golden_text("cell-sorted-missing-cb", "cell")
     monkeypatch.delenv("SCT_GBAM_MAX_DEVICE_BYTES")
     same_as_host(path, "cell")  # the cap gone, the device decodes it again
+
+
+def _windows(path, mode, **kw):
+    t = {}
+    got = gbam.decode(path, mode, timings=t, **kw)
+    return got, t.get("windows")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", [40_000, 150_000])
+@pytest.mark.parametrize("mode", ["cell", "gene"])
+def test_windowed_decode_matches_host(tmp_path, monkeypatch, window, mode):
+    """Bounded device memory: with SCT_GBAM_WINDOW_BYTES far below the payload the
+    file is decoded in >= 3 windows of whole members -- carried records cut by a window's end,
+    tables grown between windows, strings moved to the arena -- and the columns and dictionaries
+    still equal the host decoder's.  Members of 997 bytes also cut records in every window."""
+    raw = payload(os.path.join(GOLD, "cell-sorted-missing-cb.bam"))
+    for name, block in (("big", 65280), ("small", 997)):
+        path = str(tmp_path / (name + ".bam"))
+        rebgzf(raw, path, level=6, block=block)
+        monkeypatch.setenv("SCT_GBAM_WINDOW_BYTES", str(window))
+        got, nw = _windows(path, mode)
+        assert got is not None, gbam.last_error()
+        assert nw >= 3, nw
+        want, want_names = host(path, mode)
+        cols, names = got
+        assert names == want_names
+        for c, a in want.items():
+            assert np.array_equal(cols[c].cpu().numpy().view(a.dtype), a), (name, mode, c)
+        monkeypatch.delenv("SCT_GBAM_WINDOW_BYTES")
+        assert gbam.inflate(path) == raw  # one window again: the payload is resident
+
+
+@pytest.mark.gpu
+def test_windowed_count_mode_matches_host(tmp_path, monkeypatch):
+    """Count mode across windows: the query-name head of each window's first record compares with
+    the previous window's last record (carried with the cut one)."""
+    raw = payload(os.path.join(H.GOLDEN, "count", "synth_b_qname.bam"))
+    path = str(tmp_path / "q.bam")
+    rebgzf(raw, path, level=6, block=997)
+    monkeypatch.setenv("SCT_GBAM_WINDOW_BYTES", "6000")
+    t = {}
+    got = gbam.decode(path, "count", tags=("CB", "UB", "GE"), timings=t)
+    assert got is not None, gbam.last_error()
+    assert t["windows"] >= 3
+    want, want_names = bamnative.decode(path, "count", tags=("CB", "UB", "GE"))
+    cols, names = got
+    assert names == [list(n) for n in want_names]
+    for c in gbam.COUNT_COLUMNS:
+        assert np.array_equal(cols[c].cpu().numpy(), want[c]), c
+
+
+@pytest.mark.gpu
+def test_windowed_gatherer_matches_reference(tmp_path, monkeypatch):
+    """The drop-in through windows: GatherCellMetrics' CSV is still the reference's."""
+    from sctools_amd.metrics import GatherCellMetrics, GatherGeneMetrics
+
+    monkeypatch.setenv("SCT_GBAM_WINDOW_BYTES", "100000")
+    for bam in ("cell-sorted-missing-cb", "small-gene-sorted"):
+        for cls, kind in ((GatherCellMetrics, "cell"), (GatherGeneMetrics, "gene")):
+            stem = str(tmp_path / (bam + kind))
+            cls(os.path.join(GOLD, bam + ".bam"), stem, compress=False).extract_metrics()
+            assert open(stem + ".csv").read() == H.golden_text(bam, kind), (bam, kind)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_parts", [2, 3, 7])
+@pytest.mark.parametrize("window", [None, 30_000])
+def test_parts_decode_matches_host(tmp_path, monkeypatch, n_parts, window):
+    """devices=N decodes part p of the file on device p: byte-balanced member
+    ranges, each part's first record proven against the previous part's walk, dictionaries merged
+    and ids renumbered.  Concatenated in part order, the parts equal the host decoder's columns; the
+    shards re-cut at cell runs keep every cell on one shard.  All parts on device 0 here (one GPU)."""
+    from sctools_amd import columnar
+
+    raw = payload(os.path.join(GOLD, "cell-sorted-missing-cb.bam"))
+    path = str(tmp_path / "p.bam")
+    rebgzf(raw, path, level=6, block=997)
+    if window:
+        monkeypatch.setenv("SCT_GBAM_WINDOW_BYTES", str(window))
+    t = {}
+    got = gbam.decode_parts(path, "cell", ["cuda:0"] * n_parts, timings=t)
+    assert got is not None, gbam.last_error()
+    assert len(t["parts"]) == n_parts and min(t["parts"]) > 0, t["parts"]
+    shards, names = got
+    want, want_names = host(path, "cell")
+    assert [d.names for d in names] == want_names
+    for c, a in want.items():
+        g = np.concatenate([sh[c].cpu().numpy().view(a.dtype) for sh in shards])
+        assert np.array_equal(g, a), c
+    sc = columnar.ShardedColumns(columnar.cut_runs(shards, "cell"), *names)
+    assert sc.n == want["cell"].shape[0]
+    heads = [sh["cell"].cpu().numpy() for sh in sc.shards if sh["cell"].shape[0]]
+    for a, b in zip(heads, heads[1:]):
+        assert a[-1] != b[0]  # no cell run spans two shards
+    assert np.array_equal(sc.host().arrays["cell"], want["cell"])
+    idx = np.array([0, 5, sc.n // 2, sc.n - 1])
+    assert np.array_equal(sc.column_at("gene", idx), want["gene"][idx])
