@@ -55,23 +55,28 @@ __device__ __forceinline__ uint32_t u32(const uint8_t* U, uint64_t p) {
 // k_walk's agreement check decides
 // open_end: U ends inside a record that continues in the next window (a chain reaching the end
 // cannot be disproved)
+// (every field is checked before a record running past U is accepted, so an arbitrary offset whose
+// first four bytes read as a huge block_size does not pass for a start at an open end; U has kPad
+// readable bytes past ulen)
 __device__ bool plausible(const uint8_t* U, uint64_t ulen, uint64_t p, bool open_end) {
   for (int j = 0; j < 4; j++) {
     if (p == ulen) return true;
-    if (p + 36 > ulen) return open_end;
+    if (p + 36 > ulen) return open_end && j > 0;
     const uint32_t bs = u32(U, p);
-    if (bs < 33) return false;
-    if (p + 4 + bs > ulen) return open_end;
+    if (bs < 33 || bs > (1u << 28)) return false;
     const uint64_t d = p + 4;
     if ((int32_t)u32(U, d) < -1 || (int32_t)u32(U, d + 4) < -1) return false;
     const uint32_t lrn = U[d + 8];
-    if (lrn == 0 || 32 + lrn > bs || U[d + 32 + lrn - 1] != 0) return false;
+    if (lrn == 0 || 32 + lrn > bs) return false;
+    if (d + 32 + lrn > ulen) return open_end && j > 0;
+    if (U[d + 32 + lrn - 1] != 0) return false;
     for (uint32_t q = 0; q + 1 < lrn; q++) {
       const uint32_t c = U[d + 32 + q];
       if (c < 33 || c > 126) return false;
     }
     const uint64_t need = 32ull + lrn + 4ull * u16(U, d + 12) + (u32(U, d + 16) + 1ull) / 2 + u32(U, d + 16);
     if (need > bs) return false;
+    if (p + 4 + bs > ulen) return open_end;  // the rest of this record is in the next window
     p = d + bs;
   }
   return true;

@@ -77,40 +77,46 @@ __device__ __forceinline__ uint64_t gene_payload8(uint32_t g, uint32_t f, uint32
 // tile (kFull: block-uniform, so no per-lane branches and no wait after every load), element
 // by element with zeros past n in the last tile.  The columns are allocated 16-byte aligned.
 constexpr int kEmitVec = 4;  // (the rank packing below assumes 4)
-template <bool kFull, typename T>
-__device__ __forceinline__ void load_vec(const T* __restrict__ col, int64_t p0, int64_t n, T (&v)[kEmitVec]) {
-  struct alignas(sizeof(T) * kEmitVec) Vec {
-    T x[kEmitVec];
+template <bool kFull, int V, typename T>
+__device__ __forceinline__ void load_vec(const T* __restrict__ col, int64_t p0, int64_t n, T (&v)[V]) {
+  constexpr int kW = sizeof(T) * V > 16 ? 16 / (int)sizeof(T) : V;  // elements per load (<= 16 bytes)
+  struct alignas(sizeof(T) * kW) Vec {
+    T x[kW];
   };
   if constexpr (kFull) {
-    const Vec w = *reinterpret_cast<const Vec*>(col + p0);
 #pragma unroll
-    for (int k = 0; k < kEmitVec; k++) v[k] = w.x[k];
+    for (int c = 0; c < V; c += kW) {
+      const Vec w = *reinterpret_cast<const Vec*>(col + p0 + c);
+#pragma unroll
+      for (int k = 0; k < kW; k++) v[c + k] = w.x[k];
+    }
   } else {
 #pragma unroll
-    for (int k = 0; k < kEmitVec; k++) v[k] = p0 + k < n ? col[p0 + k] : (T)0;
+    for (int k = 0; k < V; k++) v[k] = p0 + k < n ? col[p0 + k] : (T)0;
   }
 }
 
-// the columns gene_emit reads for one lane's kEmitVec consecutive records
-struct EmitIn {
-  int32_t g[kEmitVec];
-  uint8_t bt[kEmitVec], xf[kEmitVec], ug[kEmitVec], ul[kEmitVec];
-  uint16_t df[kEmitVec], gg[kEmitVec], gl[kEmitVec], gs[kEmitVec];
+// the columns gene_emit reads for one lane's V consecutive records
+template <int V>
+struct EmitInV {
+  int32_t g[V];
+  uint8_t bt[V], xf[V], ug[V], ul[V];
+  uint16_t df[V], gg[V], gl[V], gs[V];
   template <bool kFull>
   __device__ __forceinline__ void load(const int32_t* __restrict__ gene, const RecCols& r,
                                        const uint16_t* __restrict__ dflags, int64_t p0, int64_t n) {
-    load_vec<kFull>(gene, p0, n, g);
-    load_vec<kFull>(r.bits, p0, n, bt);
-    load_vec<kFull>(r.xf, p0, n, xf);
-    load_vec<kFull>(r.uy_gt30, p0, n, ug);
-    load_vec<kFull>(r.uy_len, p0, n, ul);
-    load_vec<kFull>(dflags, p0, n, df);
-    load_vec<kFull>(r.gq_gt30, p0, n, gg);
-    load_vec<kFull>(r.gq_len, p0, n, gl);
-    load_vec<kFull>(r.gq_sum, p0, n, gs);
+    load_vec<kFull, V>(gene, p0, n, g);
+    load_vec<kFull, V>(r.bits, p0, n, bt);
+    load_vec<kFull, V>(r.xf, p0, n, xf);
+    load_vec<kFull, V>(r.uy_gt30, p0, n, ug);
+    load_vec<kFull, V>(r.uy_len, p0, n, ul);
+    load_vec<kFull, V>(dflags, p0, n, df);
+    load_vec<kFull, V>(r.gq_gt30, p0, n, gg);
+    load_vec<kFull, V>(r.gq_len, p0, n, gl);
+    load_vec<kFull, V>(r.gq_sum, p0, n, gs);
   }
 };
+using EmitIn = EmitInV<kEmitVec>;
 
 // One block per key-pass tile (kEmitTile = build_keys' kKTile records, input order, coalesced).
 // build_keys counted the tile's records per gene bucket and reserved the tile's range in each
@@ -165,23 +171,129 @@ __device__ __forceinline__ void gene_emit_tile(const int32_t* __restrict__ gene,
   }
 }
 
+// The narrow payloads staged in LDS (round 4): the tile's records go out in halves of
+// kEmitHalf, each counting-sorted by bucket in LDS (an atomic rank, a scan of the bucket counts)
+// and written as one contiguous run per bucket range.  Written straight from registers, the 64
+// lanes of a store hit ~64 buckets -- 64 cache lines per store instruction -- and the emit stalled
+// on issuing its stores (SQ: wait_inst 0.69, profiles/r04/a_gene_reduce_ablation/).
+#ifndef SCT_EMIT_STAGE
+#define SCT_EMIT_STAGE 4096
+#endif
+#ifndef SCT_EMIT_VEC
+#define SCT_EMIT_VEC 4
+#endif
+constexpr int kEmitHalf = SCT_EMIT_STAGE;  // records staged at a time
+constexpr int kEmitParts = kEmitTile / kEmitHalf;
+constexpr int kSVec = SCT_EMIT_VEC;  // consecutive records per lane per round
+constexpr int kEmitPer = kEmitHalf / (kBlock * kSVec);  // rounds of kSVec records per stage
+static_assert(kEmitHalf <= 4096 && kEmitTile % kEmitHalf == 0 && kEmitPer >= 1, "12-bit ranks, whole stages");
+template <bool kFull>
+__device__ __forceinline__ void gene_emit_staged(const int32_t* __restrict__ gene, const RecCols& r,
+                                                 const uint16_t* __restrict__ dflags, int64_t n, int64_t base,
+                                                 const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ toff,
+                                                 int n_buckets, uint64_t* __restrict__ pay, uint32_t* s_cnt,
+                                                 uint32_t* s_off, uint32_t* s_loc, uint64_t* s_pay, uint16_t* s_bkt,
+                                                 uint64_t* s_scan) {
+  const int t = threadIdx.x;
+  for (int i = t; i < n_buckets; i += kBlock) {
+    s_cnt[i] = 0;
+    s_off[i] = bstart[i] + toff[i];
+  }
+  __syncthreads();
+  for (int h = 0; h < kEmitParts; h++) {
+    const int64_t hb = base + (int64_t)h * kEmitHalf;
+    uint64_t pv[kEmitPer * kSVec];
+    uint32_t br[kEmitPer * kSVec];  // bucket << 12 | rank; ~0u: past n
+    // software-pipelined: round j + 1's column loads in flight while round j is ranked
+    EmitInV<kSVec> cur;
+    cur.load<kFull>(gene, r, dflags, hb + t * kSVec, n);
+#pragma unroll
+    for (int j = 0; j < kEmitPer; j++) {
+      const int64_t p0 = hb + (j * kBlock + t) * kSVec;
+      EmitInV<kSVec> nxt;
+      if (j + 1 < kEmitPer) nxt.load<kFull>(gene, r, dflags, p0 + kBlock * kSVec, n);
+#pragma unroll
+      for (int k = 0; k < kSVec; k++) {
+        const int i = j * kSVec + k;
+        br[i] = ~0u;
+        pv[i] = 0;
+        if (kFull || p0 + k < n) {
+          const uint32_t gk = (uint32_t)cur.g[k];
+          const uint32_t bk = gk / kGenesPerBucket;
+          const uint32_t f = gene_flags(cur.bt[k], cur.xf[k], cur.df[k]);
+          pv[i] = gene_payload8(gk, f, cur.ug[k], cur.ul[k], cur.gg[k], cur.gl[k], cur.gs[k]);
+          br[i] = (bk << 12) | atomicAdd(&s_cnt[bk], 1u);
+        }
+      }
+      if (j + 1 < kEmitPer) cur = nxt;
+    }
+    __syncthreads();
+    // bucket counts -> staging starts (s_loc), in chunks of kBlock buckets
+    uint64_t carry = 0;
+    for (int b0 = 0; b0 < n_buckets; b0 += kBlock) {
+      const int b = b0 + t;
+      const uint64_t c = b < n_buckets ? s_cnt[b] : 0;
+      uint64_t tot;
+      const uint64_t ex = block_exclusive_scan<uint64_t>(c, &tot, s_scan) + carry;
+      carry += tot;
+      if (b < n_buckets) s_loc[b] = (uint32_t)ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kEmitPer * kSVec; i++) {
+      if (br[i] == ~0u) continue;
+      const uint32_t q = s_loc[br[i] >> 12] + (br[i] & 0xfffu);
+      s_pay[q] = pv[i];
+      s_bkt[q] = (uint16_t)(br[i] >> 12);
+    }
+    __syncthreads();
+    const int cnt = (int)carry;
+    for (int q = t; q < cnt; q += kBlock) {
+      const uint32_t b = s_bkt[q];
+      pay[(uint64_t)s_off[b] + (uint32_t)(q - (int)s_loc[b])] = s_pay[q];
+    }
+    __syncthreads();
+    for (int i = t; i < n_buckets; i += kBlock) {
+      s_off[i] += s_cnt[i];
+      s_cnt[i] = 0;
+    }
+    __syncthreads();
+  }
+}
+
 // bstart: the bucket starts (k_gene_plan); gtoff: build_keys' per-(tile, bucket) range offsets
+// (narrow payloads: staged in LDS, gene_emit_staged, when the bucket arrays fit (staged); wide:
+// written from registers)
+constexpr int kEmitStagedBuckets = 2048;  // 3 x 8 KB of bucket arrays beside the 40 KB staging
 __global__ void __launch_bounds__(kBlock) k_gene_emit(const int32_t* __restrict__ gene, RecCols r,
                                                       const uint16_t* __restrict__ dflags, int64_t n,
                                                       const uint32_t* __restrict__ bstart,
                                                       const uint32_t* __restrict__ gtoff, int n_buckets,
-                                                      const uint32_t* __restrict__ gwide, void* __restrict__ pay) {
-  uint32_t* s_cnt = sct_dyn_lds;              // n_buckets (dynamic LDS)
-  uint32_t* s_off = sct_dyn_lds + n_buckets;  // n_buckets
+                                                      const uint32_t* __restrict__ gwide, int staged,
+                                                      void* __restrict__ pay) {
+  __shared__ uint64_t s_pay[kEmitHalf];
+  __shared__ uint16_t s_bkt[kEmitHalf];
+  __shared__ uint64_t s_scan[kWaves + 1];
+  uint32_t* s_cnt = sct_dyn_lds;                  // n_buckets each (dynamic LDS)
+  uint32_t* s_off = sct_dyn_lds + n_buckets;
+  uint32_t* s_loc = sct_dyn_lds + 2 * n_buckets;
   const int64_t base = (int64_t)blockIdx.x * kEmitTile;
   const uint32_t* toff = gtoff + (size_t)blockIdx.x * n_buckets;
   const bool full = base + kEmitTile <= n, wide = *gwide != 0;  // block-uniform
   if (wide) {
     if (full) gene_emit_tile<true, false>(gene, r, dflags, n, base, bstart, toff, n_buckets, pay, s_cnt, s_off);
     else gene_emit_tile<false, false>(gene, r, dflags, n, base, bstart, toff, n_buckets, pay, s_cnt, s_off);
-  } else {
+  } else if (!staged) {  // (more buckets than the staging's LDS allows)
     if (full) gene_emit_tile<true, true>(gene, r, dflags, n, base, bstart, toff, n_buckets, pay, s_cnt, s_off);
     else gene_emit_tile<false, true>(gene, r, dflags, n, base, bstart, toff, n_buckets, pay, s_cnt, s_off);
+  } else {
+    uint64_t* p8 = reinterpret_cast<uint64_t*>(pay);
+    if (full)
+      gene_emit_staged<true>(gene, r, dflags, n, base, bstart, toff, n_buckets, p8, s_cnt, s_off, s_loc, s_pay, s_bkt,
+                             s_scan);
+    else
+      gene_emit_staged<false>(gene, r, dflags, n, base, bstart, toff, n_buckets, p8, s_cnt, s_off, s_loc, s_pay,
+                              s_bkt, s_scan);
   }
 }
 

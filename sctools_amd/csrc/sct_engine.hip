@@ -577,9 +577,10 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     LAUNCH_SHM("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), 2 * sizeof(uint32_t) * (size_t)(L.n_buckets + 1), s,
                (const uint32_t*)gcounts, L.n_buckets, gcur, gwork, n_gwork);
     static_assert(kEmitTile == kKTile, "gene_emit tiles are the key pass's tiles (gtoff)");
+    const int staged = L.n_buckets <= kEmitStagedBuckets ? 1 : 0;
     LAUNCH_SHM_N("gene_emit", n, k_gene_emit, dim3((unsigned)cdiv(n, kEmitTile)), dim3(kBlock),
-               2 * sizeof(uint32_t) * (size_t)L.n_buckets, s, rec->gene, rc2, (const uint16_t*)dflags, n,
-               (const uint32_t*)gcur, (const uint32_t*)gtoff, L.n_buckets, (const uint32_t*)gwide, gpay);
+               (staged ? 3 : 2) * sizeof(uint32_t) * (size_t)L.n_buckets, s, rec->gene, rc2, (const uint16_t*)dflags,
+               n, (const uint32_t*)gcur, (const uint32_t*)gtoff, L.n_buckets, (const uint32_t*)gwide, staged, gpay);
     HIPCHK(hipMemsetAsync(gene_partials, 0, sizeof(int64_t) * SCT_NP * (size_t)plan->n_gene_ids, s));
     LAUNCH_N("gene_reduce", n, k_gene_reduce, dim3((unsigned)L.max_gene_work), dim3(kBlock), s, (const void*)gpay,
            (const int64_t*)gwork, (const int64_t*)n_gwork, plan->n_gene_ids, (const uint32_t*)gwide, gene_partials);

@@ -101,6 +101,7 @@ class _Handle:
         self.rc = self.L.sct_gbam_open_part(os.fsencode(path), int(part), int(n_parts), int(first_start),
                                             int(self.dev.index), ctypes.c_void_p(self.stream.cuda_stream),
                                             ctypes.byref(self.h), ctypes.byref(n))
+        self.err = last_error()  # (thread-local in the library: read on the calling thread)
         self.n = int(n.value)
 
     def bounds(self):
@@ -264,31 +265,42 @@ def decode_parts(path: str, metric_mode: str, devices, timings: Optional[dict] =
 
         each(open_one)
         for h in hs:
-            _check(h.rc)
-        if any(h.rc == HOST for h in hs):
+            if h.rc not in (OK, HOST):
+                raise OSError("device BAM decode failed (%d): %s" % (h.rc, h.err))
+        if hs[0].rc == HOST:
             return None
-        for p in range(1, P):  # part p starts where part p-1's walk lands
+        # part p starts where part p-1's walk lands: a part whose own guess disagrees (or failed
+        # from a wrong guess) is reopened there
+        for p in range(1, P):
             land = hs[p - 1].bounds()[1]
-            if hs[p].bounds()[0] != land:
+            if hs[p].rc == HOST or hs[p].bounds()[0] != land:
                 hs[p].close()
                 with torch.cuda.device(devs[p]):
                     hs[p] = _Handle(path, devs[p], p, P, first_start=land)
-                _check(hs[p].rc)
+                if hs[p].rc not in (OK, HOST):
+                    raise OSError("device BAM decode failed (%d): %s" % (hs[p].rc, hs[p].err))
                 if hs[p].rc == HOST:
                     return None
         cols: list = [None] * P
         rcs = [OK] * P
+        msgs = [""] * P
 
         def parse_one(p):
             h = hs[p]
-            cols[p] = {c: torch.empty(h.n, dtype=_TORCH_DTYPES[c], device=h.dev) for c in N.RECORD_COLUMNS}
+            try:
+                cols[p] = {c: torch.empty(h.n, dtype=_TORCH_DTYPES[c], device=h.dev) for c in N.RECORD_COLUMNS}
+            except torch.cuda.OutOfMemoryError:
+                rcs[p] = HOST
+                return
             if h.n:
                 ptrs = (ctypes.c_void_p * len(N.RECORD_COLUMNS))(*[cols[p][c].data_ptr() for c in N.RECORD_COLUMNS])
                 rcs[p] = h.L.sct_gbam_parse(h.h, _MODES[metric_mode], ptrs)
+                msgs[p] = last_error()
 
         each(parse_one)
-        for rc in rcs:
-            _check(rc)
+        for rc, msg in zip(rcs, msgs):
+            if rc not in (OK, HOST):
+                raise OSError("device BAM decode failed (%d): %s" % (rc, msg))
         if any(rc == HOST for rc in rcs):
             return None
         L = load()
