@@ -196,14 +196,51 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// SCT_WF_PAIRS: how record q's reciprocal pair reaches the chain lanes.  0: four v_readlane per
+// record (round 3); 1: one broadcast ds_read_b128 from a per-wave LDS row; 2 (round 4): no transfer
+// at all -- every row of 16 lanes computes the pairs of the same 16 records, and the two FP64 FMAs
+// of the division read record q's pair from lane q of their own row as a DPP operand
+// (v_fmac_f64_dpp row_newbcast:q): the lone wave that carries the longest entity is issue-bound,
+// and the readlanes were 4 of its 11 instructions per record.  t = RN(l d) is taken as
+// fma(l, d, +0), which rounds the same product once (a zero product gives +0 instead of -0 only
+// where the next fma's sum is +0 either way).
+#ifndef SCT_WF_PAIRS
+#define SCT_WF_PAIRS 2
+#endif
+#define SCT_WF_DPP_CASE(Q)                                                                                     \
+  case Q:                                                                                                      \
+    if (Q == 0)                                                                                                \
+      asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:" #Q " row_mask:0xf bank_mask:0xf"     \
+                   : "+v"(t)                                                                                   \
+                   : "v"(y), "v"(d));                                                                          \
+    else                                                                                                       \
+      asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #Q " row_mask:0xf bank_mask:0xf"                  \
+                   : "+v"(t)                                                                                   \
+                   : "v"(y), "v"(d));                                                                          \
+    break;
+// t += y[lane q of this row] * d (q a compile-time constant after unrolling: the switch folds).  y is
+// written at q == 0 only (a sub-chunk's pairs): the s_nop there covers the DPP read-after-VALU-write
+// hazard on it.
+__device__ __forceinline__ void fmac_row_bcast(double& t, double y, double d, int q) {
+  switch (q) {
+    SCT_WF_DPP_CASE(0) SCT_WF_DPP_CASE(1) SCT_WF_DPP_CASE(2) SCT_WF_DPP_CASE(3) SCT_WF_DPP_CASE(4)
+    SCT_WF_DPP_CASE(5) SCT_WF_DPP_CASE(6) SCT_WF_DPP_CASE(7) SCT_WF_DPP_CASE(8) SCT_WF_DPP_CASE(9)
+    SCT_WF_DPP_CASE(10) SCT_WF_DPP_CASE(11) SCT_WF_DPP_CASE(12) SCT_WF_DPP_CASE(13) SCT_WF_DPP_CASE(14)
+    SCT_WF_DPP_CASE(15)
+    default: break;
+  }
+}
+#undef SCT_WF_DPP_CASE
 template <bool kCell>
 __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __restrict__ ent_start, int64_t n_ent,
                                                            int64_t n, const uint32_t* __restrict__ order,
                                                            WelfordCtl* __restrict__ ctl,
                                                            const double* __restrict__ xs, double* __restrict__ out_f) {
   constexpr int ns = kCell ? 4 : 3;
+  __shared__ double2 s_y_all[kWaves][kWave];
   const int lane = threadIdx.x & (kWave - 1);
   const int st = lane & 3;
+  double2* s_y = s_y_all[threadIdx.x / kWave];
   const uint32_t n_big = ctl->n_big;
   const uint32_t n_groups = (n_big + kWfGroup - 1) / kWfGroup;
   while (true) {
@@ -242,6 +279,11 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
       const double kd = (double)(c0 + lane + 1);
       const double yh = 1.0 / kd;
       const double yl = __fma_rn(-kd, yh, 1.0) * yh;
+      if (SCT_WF_PAIRS == 1) {
+        __builtin_amdgcn_wave_barrier();  // the previous chunk's reads of the row are done (in order per wave)
+        s_y[lane] = make_double2(yh, yl);
+        __builtin_amdgcn_wave_barrier();
+      }
 #pragma unroll
       for (int hb = 0; hb < kWave / kWfBatch; hb++) {
         const int64_t c = c0 + hb * kWfBatch;
@@ -265,9 +307,42 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
         // waves issue in order, and after the mean add the M2 sub -> mul -> add would otherwise hold
         // the next record's ops behind two more dependent FP64 latencies (12.9 against 14.3 ms
         // at config 2, profiles/r03/s_welford_m2_pipelined/).  Same operations on the same values.
+        // SCT_WF_PAIRS 2: each row's lane j holds the pair of record c + 16 i + j for the batch's
+        // sub-chunk i of 16 records
+        double yh16 = 0.0, yl16 = 0.0;
         const auto update = [&](int q, bool act, bool fast) {
           const double x = xb[q];
-          const double h = readlane_f64(yh, hb * kWfBatch + q), l = readlane_f64(yl, hb * kWfBatch + q);
+          if (SCT_WF_PAIRS == 2) {
+            if ((q & 15) == 0) {
+              const double kq = (double)(c + q + (lane & 15) + 1);
+              yh16 = 1.0 / kq;
+              yl16 = __fma_rn(-kq, yh16, 1.0) * yh16;
+            }
+            double delta = x - mean;
+            double d2 = px - mean;
+            asm volatile("" : "+v"(delta), "+v"(d2));
+            double t = 0.0;
+            fmac_row_bcast(t, yl16, delta, q & 15);  // RN(l delta)
+            double p2 = pdelta * d2;
+            asm volatile("" : "+v"(t), "+v"(p2));
+            fmac_row_bcast(t, yh16, delta, q & 15);  // RN(h delta + RN(l delta)) = RN(delta / k)
+            double pm2 = m2 + p2;
+            asm volatile("" : "+v"(t), "+v"(pm2));
+            m2 = fast || pact ? pm2 : m2;
+            const double nm = mean + t;
+            mean = act ? nm : mean;
+            pdelta = delta, px = x, pact = act;
+            return;
+          }
+          double h, l;
+          if (SCT_WF_PAIRS == 1) {
+            const double2 y = s_y[hb * kWfBatch + q];  // one broadcast read (every lane, one address)
+            h = y.x;
+            l = y.y;
+          } else {
+            h = readlane_f64(yh, hb * kWfBatch + q);
+            l = readlane_f64(yl, hb * kWfBatch + q);
+          }
           // the issue order is pinned by empty asm statements (the scheduler would put the M2 ops
           // back between two records): the two subs, the two muls, the fma and the M2 add, then
           // the mean add

@@ -24,7 +24,10 @@ namespace sct {
 
 // payloads per reduce work item (each item ends with up to kGenesPerBucket x 39 global atomics into
 // the gene rows; 65536-payload items measured 0.87-0.89 ms against 0.85 at config 2)
-constexpr int kGeneChunk = 16384;
+#ifndef SCT_GENE_CHUNK
+#define SCT_GENE_CHUNK 16384
+#endif
+constexpr int kGeneChunk = SCT_GENE_CHUNK;
 constexpr int kGeneSub = 2048;  // 16-byte payloads sorted in LDS at a time (32 KB)
 constexpr int kGeneCnt = 1 + kGeneFlags;  // n_reads + flag counts (32-bit bins)
 constexpr int kGeneCntPad = 16;

@@ -150,6 +150,12 @@ def main():
                     help="GatherGeneMetrics on a gene-sorted BAM (small-gene-sorted.bam, each record "
                          "repeated --records-per-run times, gene names renamed per replica) instead")
     ap.add_argument("--records-per-run", type=int, default=20)
+    ap.add_argument("--synth", action="store_true",
+                    help="a config-2-shaped BAM from tools/synthbam.cpp (random 16-mer cells of ~10k reads, "
+                         "30k Zipf genes in random name order, 10-mer UMIs, soft clips, CR != CB) instead of "
+                         "the replicated fixture")
+    ap.add_argument("--devices", type=int, default=0,
+                    help="also time GatherCellMetrics(devices=[0] * N): N parts decoded and computed together")
     ap.add_argument("--count", action="store_true",
                     help="CountMatrix.from_sorted_tagged_bam (CreateCountMatrix) on the cell-sorted BAM instead")
     a = ap.parse_args()
@@ -157,7 +163,18 @@ def main():
         return main_gene(a)
     if a.count:
         return main_count(a)
-    bam = a.bam or "/tmp/sct_e2e_%d.bam" % a.records
+    bam = a.bam or ("/tmp/sct_synth_%d.bam" if a.synth else "/tmp/sct_e2e_%d.bam") % a.records
+    if not os.path.exists(bam) and a.synth:
+        t0 = time.time()
+        exe = os.path.join(ROOT, "tools", "synthbam")
+        import subprocess
+
+        if not os.path.exists(exe):
+            subprocess.run(["g++", "-O2", "-fopenmp", "-o", exe, os.path.join(ROOT, "tools", "synthbam.cpp"), "-lz"],
+                           check=True)
+        subprocess.run([exe, bam, str(a.records)], check=True)
+        print("wrote %s (%.0f MB) in %.1fs" % (bam, os.path.getsize(bam) / 1e6, time.time() - t0), file=sys.stderr,
+              flush=True)
     if not os.path.exists(bam):
         t0 = time.time()
         n = make_bam(bam, a.records, a.replicas_per_cell)
@@ -173,6 +190,11 @@ def main():
     torch.cuda.init()
     dev = torch.device("cuda", 0)
     res = {"bam": bam, "bam_mb": os.path.getsize(bam) / 1e6, "float_mode": a.float_mode}
+
+    def log(what):  # progress on stderr (a long run stays visibly alive)
+        print("%s %s" % (what, json.dumps({k: v for k, v in res.items() if not isinstance(v, dict)})),
+              file=sys.stderr, flush=True)
+
     with open(bam, "rb") as f:  # page cache warm: the timed runs read memory, not the disk
         while f.read(1 << 26):
             pass
@@ -200,6 +222,7 @@ def main():
                 "csv_gz_s": t3 - t2, "total_s": t3 - t0, "records_per_s": cols.n / (t3 - t0)})
     del cols, arrays, got
     torch.cuda.empty_cache()
+    log("device path")
 
     runs = []
     for _ in range(3):
@@ -208,6 +231,21 @@ def main():
         runs.append(time.perf_counter() - t0)
     res["GatherCellMetrics_s"] = runs
     res["GatherCellMetrics_records_per_s"] = res["records"] / min(runs)
+    log("GatherCellMetrics")
+    if a.devices:
+        runs = []
+        for _ in range(2):
+            t0 = time.perf_counter()
+            G.GatherCellMetrics(bam, "/tmp/sct_e2e_cell4", float_mode=a.float_mode,
+                                devices=[0] * a.devices).extract_metrics()
+            runs.append(time.perf_counter() - t0)
+        res["GatherCellMetrics_parts_devices"] = [0] * a.devices
+        res["GatherCellMetrics_parts_s"] = runs
+        import gzip
+
+        res["parts_and_one_device_csv_identical"] = (gzip.open("/tmp/sct_e2e_cell2.csv.gz").read()
+                                                     == gzip.open("/tmp/sct_e2e_cell4.csv.gz").read())
+        log("devices")
     if a.host_decoder:
         t0 = time.perf_counter()
         G.GatherCellMetrics(bam, "/tmp/sct_e2e_cell3", float_mode=a.float_mode, gpu_decode=False).extract_metrics()
