@@ -141,6 +141,183 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __re
   }
 }
 
+// ---- onesweep (round 4): every pass's digit histogram in one read, tile offsets by look-back ----
+// k_radix_hist_all counts the digits of all passes at once (the histogram of a digit is the same
+// in every pass's input order), k_radix_bases turns them into each pass's digit starts, and each
+// pass is one kernel: a block takes the next tile by ticket, ranks it as k_radix_downsweep does,
+// and finds its output offset per digit by decoupled look-back over the earlier tiles' published
+// counts (status words: 2 flag bits + a 30-bit count; kLbAgg = the tile's own count, kLbPre = the
+// inclusive prefix) -- no per-tile count matrix, no upsweep pass and no device-wide scan.
+// Tickets are handed out in block start order, so a tile only ever waits on tiles whose blocks
+// have started (forward progress without co-residency).
+constexpr uint32_t kLbAgg = 1u << 30, kLbPre = 2u << 30, kLbVal = (1u << 30) - 1u;
+constexpr int kMaxPasses = 8;
+constexpr int kHistAllBlocks = 2048;
+#ifndef SCT_LOOKAHEAD
+#define SCT_LOOKAHEAD 8
+#endif
+constexpr int kLookAhead = SCT_LOOKAHEAD;
+
+__global__ void __launch_bounds__(kBlock) k_radix_hist_all(const uint64_t* __restrict__ keys, int64_t n, int passes,
+                                                           uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t h[kMaxPasses][kRadix];
+  for (int i = threadIdx.x; i < kMaxPasses * kRadix; i += kBlock) (&h[0][0])[i] = 0;
+  __syncthreads();
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p += (int64_t)gridDim.x * kBlock) {
+    const uint64_t k = keys[p];
+    for (int ps = 0; ps < passes; ps++) atomicAdd(&h[ps][(k >> (ps * kRadixBits)) & (kRadix - 1)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < passes * kRadix; i += kBlock) {
+    const uint32_t c = (&h[0][0])[i];
+    if (c) atomicAdd(&ghist[i], c);
+  }
+}
+
+// gbase[ps][d] = exclusive prefix of ghist[ps][.] (one block, kRadix == kBlock)
+__global__ void __launch_bounds__(kBlock) k_radix_bases(const uint32_t* __restrict__ ghist, int passes,
+                                                        uint32_t* __restrict__ gbase) {
+  __shared__ uint64_t s_scan[kWaves + 1];
+  for (int ps = 0; ps < passes; ps++) {
+    uint64_t tot;
+    const uint64_t ex = block_exclusive_scan<uint64_t>((uint64_t)ghist[ps * kRadix + threadIdx.x], &tot, s_scan);
+    gbase[ps * kRadix + threadIdx.x] = (uint32_t)ex;
+  }
+}
+
+__device__ __forceinline__ uint32_t lb_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(kBlock) k_radix_onesweep(const uint64_t* __restrict__ keys_in,
+                                                           const uint32_t* __restrict__ vals_in,
+                                                           uint64_t* __restrict__ keys_out,
+                                                           uint32_t* __restrict__ vals_out, int64_t n, int shift,
+                                                           const uint32_t* __restrict__ gbase,
+                                                           uint32_t* __restrict__ status,
+                                                           uint32_t* __restrict__ ticket) {
+  __shared__ uint64_t s_keys[kSortTile];
+  __shared__ uint32_t s_vals[kSortTile];
+  __shared__ uint32_t s_whist[kWaves][kRadix];
+  __shared__ uint32_t s_dstart[kRadix];
+  __shared__ uint32_t s_goff[kRadix];
+  __shared__ uint64_t s_scan[kWaves + 1];
+  __shared__ uint32_t s_tile;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+  for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_whist[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const int64_t base = (int64_t)tile * kSortTile;
+  const int tile_n = (int)((n - base) < kSortTile ? (n - base) : kSortTile);
+
+  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  uint64_t k[kSortItems];
+  uint32_t v[kSortItems];
+  uint16_t rank[kSortItems];
+  uint8_t dig[kSortItems];
+#pragma unroll
+  for (int j = 0; j < kSortItems; j++) {
+    const int q = wid * (kSortItems * kWave) + j * kWave + lane;
+    const int64_t p = base + q;
+    if (q < tile_n) {
+      k[j] = keys_in[p];
+      v[j] = vals_in[p];
+    } else {
+      k[j] = ~0ull;  // padding: digit 255, ranked after every real item, never written
+      v[j] = 0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kSortItems; j++) {
+    const uint32_t d = (uint32_t)(k[j] >> shift) & (kRadix - 1);
+    dig[j] = (uint8_t)d;
+    uint64_t peers = ~0ull;
+#pragma unroll
+    for (int bitn = 0; bitn < kRadixBits; bitn++) {
+      const uint64_t m = __ballot((d >> bitn) & 1u);
+      peers &= ((d >> bitn) & 1u) ? m : ~m;
+    }
+    const int leader = __ffsll((unsigned long long)peers) - 1;
+    const uint32_t below = (uint32_t)__popcll(peers & lt);
+    uint32_t bse = 0;
+    if (lane == leader) {
+      bse = s_whist[wid][d];
+      s_whist[wid][d] = bse + (uint32_t)__popcll(peers);
+    }
+    bse = (uint32_t)__shfl((int)bse, leader);
+    rank[j] = (uint16_t)(bse + below);
+  }
+  __syncthreads();
+  {
+    const int d = threadIdx.x;
+    uint32_t run = 0;
+    uint32_t pre[kWaves];
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+      pre[w] = run;
+      run += s_whist[w][d];
+    }
+    // the padding of a partial last tile was counted in digit 255: only real items are published
+    const uint32_t real = (d == kRadix - 1) ? run - (uint32_t)(kSortTile - tile_n) : run;
+    uint32_t* st = status + (size_t)tile * kRadix + d;
+    uint32_t excl = 0;
+    if (tile == 0) {
+      lb_store(st, kLbPre | real);
+    } else {
+      lb_store(st, kLbAgg | real);
+      // kLookAhead predecessors' words loaded together per step (their latencies overlap);
+      // consumed in order up to the first unpublished one (retried) or an inclusive prefix
+      int64_t j = (int64_t)tile - 1;
+      while (true) {
+        uint32_t w[kLookAhead];
+#pragma unroll
+        for (int u = 0; u < kLookAhead; u++)
+          w[u] = j - u >= 0 ? lb_load(status + (size_t)(j - u) * kRadix + d) : kLbPre;
+        int u = 0;
+        bool done = false;
+#pragma unroll
+        for (int v = 0; v < kLookAhead; v++) {
+          if (u != v || done) continue;  // (a gap stopped the scan)
+          if (!(w[v] & (kLbAgg | kLbPre))) continue;
+          excl += w[v] & kLbVal;
+          done = (w[v] & kLbPre) != 0;
+          u = v + 1;
+        }
+        if (done) break;
+        j -= u;
+        if (u == 0) __builtin_amdgcn_s_sleep(1);
+      }
+      lb_store(st, kLbPre | (excl + real));
+    }
+    s_goff[d] = gbase[d] + excl;
+    uint64_t tot;
+    const uint64_t ds = block_exclusive_scan<uint64_t>((uint64_t)run, &tot, s_scan);
+    s_dstart[d] = (uint32_t)ds;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) s_whist[w][d] = (uint32_t)ds + pre[w];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSortItems; j++) {
+    const uint32_t lp = s_whist[wid][dig[j]] + rank[j];
+    s_keys[lp] = k[j];
+    s_vals[lp] = v[j];
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < tile_n; q += kBlock) {
+    const uint64_t kk = s_keys[q];
+    const uint32_t d = (uint32_t)(kk >> shift) & (kRadix - 1);
+    const uint64_t o = (uint64_t)s_goff[d] + (uint32_t)(q - (int)s_dstart[d]);
+    keys_out[o] = kk;
+    vals_out[o] = s_vals[q];
+  }
+}
+
 struct SortBuffers {
   uint64_t *ka, *kb;
   uint32_t *va, *vb;
@@ -157,6 +334,33 @@ inline int radix_sort(const SortBuffers& B, int64_t n, int bits, int* which, hip
     return fail(SCT_EINVAL, "radix_sort: %lld digit counts exceed the workspace's %lld", (long long)(kRadix * tiles),
                 (long long)B.count_cap);
   int cur = 0;
+  // onesweep when the counts fit its 30-bit status words and the offsets buffer holds the
+  // histograms (ghist, gbase: kMaxPasses x kRadix each, + a ticket per pass)
+  static const char* one_env = getenv("SCT_RADIX_ONESWEEP");
+  const bool onesweep = (one_env && one_env[0] == '1') && n < (int64_t)kLbVal && passes <= kMaxPasses &&
+                        B.count_cap >= (int64_t)(2 * kMaxPasses * kRadix + kMaxPasses);
+  if (onesweep) {
+    uint32_t* ghist = B.offsets;
+    uint32_t* gbase = B.offsets + kMaxPasses * kRadix;
+    uint32_t* tickets = B.offsets + 2 * kMaxPasses * kRadix;
+    HIPCHK(hipMemsetAsync(B.offsets, 0, sizeof(uint32_t) * (2 * kMaxPasses * kRadix + kMaxPasses), s));
+    const int64_t hb = tiles < kHistAllBlocks ? tiles : kHistAllBlocks;
+    LAUNCH_N("radix_hist_all", n, k_radix_hist_all, dim3((unsigned)hb), dim3(kBlock), s, (const uint64_t*)B.ka, n,
+             passes, ghist);
+    LAUNCH("radix_bases", k_radix_bases, dim3(1), dim3(kBlock), s, (const uint32_t*)ghist, passes, gbase);
+    for (int ps = 0; ps < passes; ps++) {
+      const uint64_t* kin = cur ? B.kb : B.ka;
+      const uint32_t* vin = cur ? B.vb : B.va;
+      uint64_t* kout = cur ? B.ka : B.kb;
+      uint32_t* vout = cur ? B.va : B.vb;
+      HIPCHK(hipMemsetAsync(B.counts, 0, sizeof(uint32_t) * (size_t)kRadix * (size_t)tiles, s));
+      LAUNCH_N("radix_onesweep", n, k_radix_onesweep, dim3((unsigned)tiles), dim3(kBlock), s, kin, vin, kout, vout, n,
+               ps * kRadixBits, (const uint32_t*)(gbase + ps * kRadix), B.counts, tickets + ps);
+      cur ^= 1;
+    }
+    *which = cur;
+    return SCT_OK;
+  }
   for (int ps = 0; ps < passes; ps++) {
     const int shift = ps * kRadixBits;
     const uint64_t* kin = cur ? B.kb : B.ka;

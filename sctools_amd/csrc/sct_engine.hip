@@ -934,7 +934,11 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
     uint32_t* tctl = at<uint32_t>(workspace, L.tctl);
     HIPCHK(hipMemsetAsync(tctl, 0, 2 * sizeof(uint32_t), s));
     uint32_t* pos_of = at<uint32_t>(workspace, L.recs2);  // the row buffer is free on this path
-    LAUNCH("tag_ties", k_tie_wave, grid, dim3(kBlock), s, keys, perm, tiebreak, n, longs, tctl);
+    if (SCT_TIE_V2) {
+      LAUNCH("tag_ties", k_tie_wave2, grid, dim3(kBlock), s, keys, perm, tiebreak, n, longs, tctl);
+    } else {
+      LAUNCH("tag_ties", k_tie_wave, grid, dim3(kBlock), s, keys, perm, tiebreak, n, longs, tctl);
+    }
     uint32_t h[2] = {0, 0};
     if (int rb = readback(h, tctl, sizeof(h), s)) return rb;
     if (h[0] > 0) {  // runs longer than kTieShort: (run, tiebreak) radix sort of their records

@@ -344,6 +344,118 @@ __device__ __forceinline__ void tie_serial(const uint64_t* __restrict__ keys, ui
     if (i < L) perm[p + i] = (uint32_t)v[i];
 }
 
+// Round 4 (SCT_TIE_V2): runs inside the wave are sorted by odd-even transposition over their lanes
+// (one compare-exchange round per record of the longest such run; most runs are 2-3 records, the
+// 64-lane bitonic network is kept for waves with a run longer than kTieRounds), and the run crossing
+// the wave's end is finished by the whole wave: lanes 0..kTieShort-1 load the next keys (a halo),
+// the run's records are gathered one per lane and sorted by a 16-lane bitonic network -- instead of
+// one lane walking the run with dependent loads (tie_serial, kept for runs longer than kTieShort).
+#ifndef SCT_TIE_V2
+#define SCT_TIE_V2 1
+#endif
+constexpr int kTieRounds = 8;
+
+__device__ __forceinline__ void tie_bitonic64(uint64_t& key, uint32_t& idx, int lane) {
+#pragma unroll
+  for (int size = 2; size <= kWave; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint64_t ok = __shfl_xor(key, stride);
+      const uint32_t ov = (uint32_t)__shfl_xor((int)idx, stride);
+      const bool asc = (lane & size) == 0 || size == kWave;
+      const bool low = (lane & stride) == 0;
+      const bool take = (low == asc) ? (ok < key) : (ok > key);
+      key = take ? ok : key;
+      idx = take ? ov : idx;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_tie_wave2(const uint64_t* __restrict__ keys, uint32_t* __restrict__ perm,
+                                                      const int32_t* __restrict__ tie, int64_t n,
+                                                      uint4* __restrict__ longs, uint32_t* __restrict__ ctl) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t p0 = p - lane;
+  const bool valid = p < n;
+  const uint64_t k = valid ? keys[p] : 0ull;
+  // the halo: the keys after the wave's last position (for the run crossing its end)
+  const int64_t ph = p0 + kWave + lane;
+  const uint64_t hk = (lane < kTieShort && ph < n) ? keys[ph] : 0ull;
+  uint32_t idx = valid ? perm[p] : 0u;
+  uint64_t kp = __shfl_up(k, 1), kn = __shfl_down(k, 1);
+  if (lane == 0) kp = (p > 0 && valid) ? keys[p - 1] : ~k;
+  if (lane == kWave - 1) kn = (p + 1 < n) ? keys[p + 1] : ~k;
+  const bool head = !valid || k != kp;
+  const bool tail = !valid || p + 1 >= n || k != kn;
+  const uint64_t H = __ballot(head), T = __ballot(tail);
+  const uint64_t upto = lane == kWave - 1 ? ~0ull : ((2ull << lane) - 1);
+  const uint64_t from = ~((1ull << lane) - 1);
+  const uint64_t hs = H & upto, ts = T & from;
+  const int s0 = hs ? 63 - __clzll((long long)hs) : -1;  // first lane of the lane's run, if in this wave
+  const int s1 = ts ? __ffsll((unsigned long long)ts) - 1 : -1;  // last lane of the run, if in this wave
+  const bool need = valid && s0 >= 0 && s1 >= 0 && s1 > s0;
+  if (__ballot(need)) {
+    const uint32_t t = need ? (uint32_t)tie[idx] : 0u;
+    int len = need ? s1 - s0 + 1 : 0;
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+      const int o = __shfl_xor(len, off);
+      len = o > len ? o : len;
+    }
+    if (len <= kTieRounds) {
+      // (tiebreak, lane): ties keep input order (the radix sort is stable)
+      uint64_t key = ((uint64_t)t << 32) | (uint32_t)lane;
+      const int r = lane - s0;  // position inside the run (need lanes)
+      for (int i = 0; i < len; i++) {
+        const bool up = ((r ^ i) & 1) == 0;  // pairs (r, r + 1) with r = i mod 2
+        const int partner = up ? lane + 1 : lane - 1;
+        const uint64_t ok = __shfl(key, partner & (kWave - 1));
+        const uint32_t ov = (uint32_t)__shfl((int)idx, partner & (kWave - 1));
+        const bool in = need && partner >= s0 && partner <= s1;
+        const bool take = in && (up ? (ok < key) : (ok > key));
+        key = take ? ok : key;
+        idx = take ? ov : idx;
+      }
+    } else {
+      uint64_t key = ((uint64_t)(need ? s0 : lane) << 58) | ((uint64_t)t << 6) | (uint64_t)lane;
+      tie_bitonic64(key, idx, lane);
+    }
+    if (need) perm[p] = idx;
+  }
+  // the run crossing the wave's end (lane 63 is not a tail) and starting in this wave
+  if (!((T >> (kWave - 1)) & 1ull) && H) {
+    const int h = 63 - __clzll((long long)H);
+    const uint64_t kl = __shfl(k, kWave - 1);
+    const uint64_t same = __ballot(lane < kTieShort && ph < n && hk == kl);
+    const int ext = (int)__builtin_ctzll(~same);  // halo records continuing the run
+    const int L = kWave - h + ext;
+    if (L > kTieShort || ext == kTieShort) {  // a long run (or one that may be): the serial path
+      if (lane == h) tie_serial(keys, perm, tie, n, p, longs, ctl);
+    } else {
+      const int64_t q = p0 + h + lane;  // record `lane` of the run
+      const bool mine = lane < L;
+      const uint32_t qi = mine ? perm[q] : 0u;
+      uint64_t key = mine ? (((uint64_t)(uint32_t)tie[qi] << 32) | (uint32_t)lane) : ~0ull;
+      uint32_t qv = qi;
+#pragma unroll
+      for (int size = 2; size <= kTieShort; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          const uint64_t ok = __shfl_xor(key, stride);
+          const uint32_t ov = (uint32_t)__shfl_xor((int)qv, stride);
+          const bool asc = (lane & size) == 0 || size == kTieShort;
+          const bool low = (lane & stride) == 0;
+          const bool take = (low == asc) ? (ok < key) : (ok > key);
+          key = take ? ok : key;
+          qv = take ? ov : qv;
+        }
+      }
+      if (mine) perm[q] = qv;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_tie_wave(const uint64_t* __restrict__ keys, uint32_t* __restrict__ perm,
                                                      const int32_t* __restrict__ tie, int64_t n,
                                                      uint4* __restrict__ longs, uint32_t* __restrict__ ctl) {
