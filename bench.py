@@ -58,6 +58,9 @@ ALG_BYTES = {
     "tag_row_hist": 4,       # config 5, per pass: read the cell key
     "tag_pack": 64,          # tag sort with a tiebreak: read the 32-byte SoA record, write it packed
     "tag_keys": 28,          # read the packed record's key words (16), write key 8 + index 4
+    "tag_pack_keys": 80,     # read the SoA record (32) + tiebreak (4), write the packed row (32) + key 8 + index 4
+    "radix_onesweep": 24,    # (opt-in onesweep) read key 8 + value 4, write key 8 + value 4
+    "radix_hist_all": 8,
     "tag_unpack": 64,        # gather the packed record (32), write the SoA columns (32)
     "radix_downsweep": 24,   # global-sort path: read key 8 + value 4, write key 8 + value 4
     "radix_upsweep": 8,
@@ -72,7 +75,8 @@ ALG_BYTES = {
 # covering several kernels gets their dispatch-weighted mean bytes per launch
 PMC_NAMES = {"build_keys": ["build_keys_run"], "heads": ["heads4", "heads"],
              "scan": ["scan_wide", "scan_reduce", "scan_small", "scan_apply"],
-             "tag_pack": ["pack"], "tag_keys": ["field_keys", "round_keys"], "tag_ties": ["tie_wave"],
+             "tag_pack": ["pack"], "tag_keys": ["field_keys", "round_keys"], "tag_ties": ["tie_wave", "tie_wave2"],
+             "tag_pack_keys": ["pack_field_keys"],
              "tag_long_keys": ["long_keys"], "tag_long_scatter": ["long_scatter"], "tag_unpack": ["unpack"],
              "tag_row_hist": ["row_hist"], "tag_row_scatter": ["row_scatter"]}
 

@@ -631,6 +631,49 @@ __global__ void k_pack(const uint8_t* __restrict__ U, const uint8_t* __restrict_
   const uint64_t s = ent_off(e), o = boff[i];
   for (uint32_t k = 0; k < ent_len(e); k++) out[o + k] = src[s + k];
 }
+// Dictionaries ranked on the device (round 4): a string of <= 16 bytes compares in Python's order
+// (code points = bytes for the ASCII the device path admits) exactly as its big-endian, zero-padded
+// 16-byte key (no dictionary string holds a NUL), so two stable 64-bit radix sorts (low word, then
+// high) give the ranks.  *too_long: some string is longer (the host sort ranks that dictionary).
+__global__ void k_strkey(const uint8_t* __restrict__ U, const uint8_t* __restrict__ A,
+                         const uint64_t* __restrict__ uent, uint32_t n, uint64_t* __restrict__ khi,
+                         uint64_t* __restrict__ klo, uint32_t* __restrict__ idx, uint32_t* __restrict__ too_long) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long e = uent[i];
+  const uint32_t len = ent_len(e);
+  if (len > 16) atomicOr(too_long, 1u);
+  const uint8_t* src = ent_src(e, U, A) + ent_off(e);
+  uint64_t hi = 0, lo = 0;
+  for (uint32_t k = 0; k < 16 && k < len; k++) {
+    const uint64_t b = src[k];
+    if (k < 8)
+      hi |= b << (56 - 8 * k);
+    else
+      lo |= b << (56 - 8 * (k - 8));
+  }
+  khi[i] = hi;
+  klo[i] = lo;
+  idx[i] = i;
+}
+__global__ void k_gather_key(const uint64_t* __restrict__ key, const uint32_t* __restrict__ idx, uint32_t n,
+                             uint64_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = key[idx[i]];
+}
+// ranked order -> rank of every dense id, and the entries / lengths in ranked order
+__global__ void k_rank_order(const uint32_t* __restrict__ order, const uint64_t* __restrict__ uent, uint32_t n,
+                             int32_t hn, int32_t* __restrict__ rank, uint64_t* __restrict__ uent2,
+                             uint32_t* __restrict__ ulen2) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint32_t i = order[r];
+  rank[i] = (int32_t)r + hn;
+  const unsigned long long e = uent[i];
+  uent2[r] = e;
+  ulen2[r] = ent_len(e);
+}
+
 __global__ void k_remap(int32_t* __restrict__ col, uint64_t n, const uint32_t* __restrict__ dense,
                         const int32_t* __restrict__ rank) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -751,6 +794,24 @@ bool header_end(const uint8_t* f, const std::vector<Block>& blocks, uint64_t* H)
 }
 
 // Python's sorted() on the strings, the missing value first: rank of each distinct string
+// The mapping's page-table entries made in parallel (a large file in the page cache): the member
+// scan below and the copies to the device then run without a page fault every few members.
+void prefault(const uint8_t* f, uint64_t fsize) {
+  constexpr uint64_t kPage = 4096, kMin = 64ull << 20;
+  if (fsize < kMin) return;
+  const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  std::atomic<uint64_t> sink{0};
+  for (unsigned t = 0; t < T; t++)
+    th.emplace_back([&, t] {
+      const uint64_t lo = fsize * t / T / kPage * kPage, hi = fsize * (t + 1) / T;
+      uint64_t acc = 0;
+      for (uint64_t o = lo; o < hi; o += kPage) acc += ((const volatile uint8_t*)f)[o];
+      sink += acc;
+    });
+  for (auto& x : th) x.join();
+}
+
 void rank_strings(const std::string& bytes, const std::vector<uint64_t>& off, int32_t has_none,
                   std::vector<int32_t>& rank, std::vector<uint32_t>& order) {
   const size_t n = off.size() - 1;
@@ -1134,6 +1195,7 @@ int open_impl(const char* path, int32_t part, int32_t n_parts, int64_t first_sta
   if (f == MAP_FAILED) return gfail(SCT_GBAM_HOST, "cannot map");
   G->f = f;
   G->fsize = fsize;
+  prefault(f, fsize);
   std::vector<Block>& blocks = G->blocks;
   if (scan_blocks(f, fsize, blocks) != SCT_BAM_OK) return gfail(SCT_GBAM_HOST, "not BGZF");
   uint64_t H = 0;
@@ -1329,6 +1391,79 @@ int parse_flags(sct_gbam* G, ParseState& P) {
   return SCT_BAM_OK;
 }
 
+// Dictionary k ranked on the device (gb::k_strkey): false if a string is longer than 16 bytes
+// (the caller ranks it on the host); else true, with *rc the result (the ranked strings and offsets
+// copied to G->dict_bytes / dict_off, column colk remapped to ranks).
+bool rank_on_device(sct_gbam* G, ParseState& P, int k, int32_t hn, DevBuf<uint64_t>& uent, DevBuf<uint32_t>& ulen,
+                    DevBuf<uint64_t>& boff, DevBuf<uint32_t>& dense, int32_t* col, DevBuf<uint8_t>& tmp, int* rc) {
+  hipStream_t st = G->st;
+  const uint32_t nu = (uint32_t)uent.n;
+  const uint64_t n = (uint64_t)G->n;
+  *rc = SCT_BAM_OK;
+  auto err = [&](hipError_t e) {
+    *rc = e == hipErrorOutOfMemory ? gfail(SCT_GBAM_HOST, "device memory exhausted: the host decoder takes the file")
+                                   : gfail(SCT_BAM_EIO, hipGetErrorString(e));
+    return true;
+  };
+#define DOK(x)                              \
+  do {                                      \
+    const hipError_t e_ = (x);              \
+    if (e_ != hipSuccess) return err(e_);   \
+  } while (0)
+  DevBuf<uint64_t> khi, klo, kt;
+  DevBuf<uint32_t> ia, ib, flag;
+  DOK(khi.alloc(nu));
+  DOK(klo.alloc(nu));
+  DOK(kt.alloc(nu));
+  DOK(ia.alloc(nu));
+  DOK(ib.alloc(nu));
+  DOK(flag.alloc(1));
+  DOK(hipMemsetAsync(flag.p, 0, sizeof(uint32_t), st));
+  hipLaunchKernelGGL(gb::k_strkey, dim3(grid(nu, 256)), dim3(256), 0, st, G->u.p, P.arena.p, uent.p, nu, khi.p,
+                     klo.p, ia.p, flag.p);
+  uint32_t too_long = 0;
+  DOK(hipMemcpyAsync(&too_long, flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  DOK(hipStreamSynchronize(st));
+  if (too_long) return false;
+  // stable LSD: by the low word, then by the high word
+  size_t tb = 0;
+  DOK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, klo.p, kt.p, ia.p, ib.p, (int)nu, 0, 64, st));
+  if (tmp.n < tb) DOK(tmp.alloc(tb));
+  DOK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, klo.p, kt.p, ia.p, ib.p, (int)nu, 0, 64, st));
+  hipLaunchKernelGGL(gb::k_gather_key, dim3(grid(nu, 256)), dim3(256), 0, st, khi.p, ib.p, nu, klo.p);
+  DOK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, klo.p, kt.p, ib.p, ia.p, (int)nu, 0, 64, st));
+  if (tmp.n < tb) DOK(tmp.alloc(tb));
+  DOK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, klo.p, kt.p, ib.p, ia.p, (int)nu, 0, 64, st));
+  // ia = the ranked order; ranks, entries and lengths in ranked order, their byte offsets
+  DevBuf<int32_t> rank_d;
+  DevBuf<uint64_t> uent2;
+  DOK(rank_d.alloc(nu));
+  DOK(uent2.alloc(nu));
+  hipLaunchKernelGGL(gb::k_rank_order, dim3(grid(nu, 256)), dim3(256), 0, st, ia.p, uent.p, nu, hn, rank_d.p,
+                     uent2.p, ulen.p);
+  DOK(exclusive_sum(ulen.p, boff.p, (uint64_t)nu + 1, st, tmp));
+  uint64_t total = 0;
+  DOK(hipMemcpyAsync(&total, boff.p + nu, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  DOK(hipStreamSynchronize(st));
+  DevBuf<uint8_t> packed;
+  DOK(packed.alloc(total));
+  hipLaunchKernelGGL(gb::k_pack, dim3(grid(nu, 256)), dim3(256), 0, st, G->u.p, P.arena.p, uent2.p, boff.p, nu,
+                     packed.p);
+  std::string& db = G->dict_bytes[k];
+  std::vector<int64_t>& dof = G->dict_off[k];
+  db.assign(total, '\0');
+  dof.assign((size_t)nu + 1 + (hn ? 1 : 0), 0);
+  if (total) DOK(hipMemcpyAsync(&db[0], packed.p, total, hipMemcpyDeviceToHost, st));
+  static_assert(sizeof(int64_t) == sizeof(uint64_t), "offsets copied as they are");
+  DOK(hipMemcpyAsync(dof.data() + (hn ? 1 : 0), boff.p, ((size_t)nu + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                     st));
+  if (n) hipLaunchKernelGGL(gb::k_remap, dim3(grid(n, 256)), dim3(256), 0, st, col, n, dense.p, rank_d.p);
+  DOK(hipGetLastError());
+  DOK(hipStreamSynchronize(st));
+#undef DOK
+  return true;
+}
+
 // The interned ids -> ranks in Python's sorted() order (None first), and the ranked strings.
 int dictionaries_impl(sct_gbam* G, ParseState& P, int32_t* const colk[3]) {
   const double t1 = now();
@@ -1360,6 +1495,13 @@ int dictionaries_impl(sct_gbam* G, ParseState& P, int32_t* const colk[3]) {
     HIPOK(hipMemsetAsync(ulen.p + nu, 0, sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_compact, dim3(grid(cap, 256)), dim3(256), 0, st, tab[k].p, cap, dense.p, uent.p, ulen.p);
     HIPOK(exclusive_sum(ulen.p, boff.p, nu + 1, st, tmp));
+    if (nu > 0 && nu < (1ull << 31)) {  // ranked on the device unless a string is longer than 16 bytes
+      int rc = 0;
+      if (rank_on_device(G, P, k, hn, uent, ulen, boff, dense, colk[k], tmp, &rc)) {
+        if (rc) return rc;
+        continue;
+      }
+    }
     std::vector<uint64_t> hoff(nu + 1);
     HIPOK(hipMemcpyAsync(hoff.data(), boff.p, (nu + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIPOK(hipStreamSynchronize(st));

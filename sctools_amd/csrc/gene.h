@@ -28,6 +28,16 @@ namespace sct {
 #define SCT_GENE_CHUNK 16384
 #endif
 constexpr int kGeneChunk = SCT_GENE_CHUNK;
+// Round 4: a bucket of >= kGeneHotBucket payloads (the Zipf head: ~55 % of the records in one
+// bucket at config 2) is reduced in items of kGeneChunkHot payloads -- each item ends with up to
+// kGenesPerBucket x 39 global atomics on the same 64 gene rows, so fewer, larger items cut that
+// write traffic; other buckets keep kGeneChunk (load balance)
+#ifndef SCT_GENE_CHUNK_HOT
+#define SCT_GENE_CHUNK_HOT 65536
+#endif
+constexpr int kGeneChunkHot = SCT_GENE_CHUNK_HOT;
+constexpr uint64_t kGeneHotBucket = 16ull * kGeneChunkHot;
+__device__ __forceinline__ uint64_t gene_chunk(uint64_t c) { return c >= kGeneHotBucket ? kGeneChunkHot : kGeneChunk; }
 constexpr int kGeneSub = 2048;  // 16-byte payloads sorted in LDS at a time (32 KB)
 constexpr int kGeneCnt = 1 + kGeneFlags;  // n_reads + flag counts (32-bit bins)
 constexpr int kGeneCntPad = 16;
@@ -315,7 +325,7 @@ __global__ void __launch_bounds__(kBlock) k_gene_plan(const uint32_t* __restrict
     uint64_t tot;
     const uint64_t beg = block_exclusive_scan<uint64_t>(c, &tot, lds) + carry;
     carry += tot;
-    const uint64_t nw = (c + kGeneChunk - 1) / kGeneChunk;
+    const uint64_t nw = (c + gene_chunk(c) - 1) / gene_chunk(c);
     uint64_t tot_w;
     const uint64_t woff = block_exclusive_scan<uint64_t>(nw, &tot_w, lds) + carry_w;
     carry_w += tot_w;
@@ -337,11 +347,12 @@ __global__ void __launch_bounds__(kBlock) k_gene_plan(const uint32_t* __restrict
       const int mid = (lo + hi + 1) / 2;
       if (s_woff[mid] <= w) lo = mid; else hi = mid - 1;
     }
-    const uint64_t b0 = (uint64_t)s_beg[lo] + (uint64_t)(w - s_woff[lo]) * kGeneChunk;
     const uint64_t e = s_beg[lo + 1];
+    const uint64_t ch = gene_chunk(e - s_beg[lo]);
+    const uint64_t b0 = (uint64_t)s_beg[lo] + (uint64_t)(w - s_woff[lo]) * ch;
     work[3 * w + 0] = lo;
     work[3 * w + 1] = (int64_t)b0;
-    work[3 * w + 2] = (int64_t)(b0 + kGeneChunk < e ? b0 + kGeneChunk : e);
+    work[3 * w + 2] = (int64_t)(b0 + ch < e ? b0 + ch : e);
   }
 }
 

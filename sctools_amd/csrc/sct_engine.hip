@@ -301,6 +301,8 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     rc = launch_hash_tile<false>(cell, gene, tgrid, s, bdesc, bent, pa, pb, n, b, partials, dflags);
   }
   if (rc) return rc;
+  // (round 4: the big buckets on a side stream beside the hash tiles measured the same step time,
+  // 5.26 ms either way, profiles/r04/e_l1fast_gbam_dicts/var/)
   if (h.n_big > 0) {
     const dim3 bgrid(h.n_big);
     const bool wide = b.k1 > kNarrowK1Bits;
@@ -911,9 +913,9 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
                 at<uint32_t>(workspace, L.vb), at<uint32_t>(workspace, L.counts), at<uint32_t>(workspace, L.offsets),
                 at<uint64_t>(workspace, L.sums), L.count_cap};
   const dim3 grid((unsigned)cdiv(n, kBlock));
-  LAUNCH_N("tag_pack", n, k_pack, grid, dim3(kBlock), s, *in, recs);
   int field_bits = 0;
   for (int i = 0; i < nf - (tiebreak ? 1 : 0); i++) field_bits += f[i].bits;
+  if (!(tiebreak && field_bits <= 64)) LAUNCH_N("tag_pack", n, k_pack, grid, dim3(kBlock), s, *in, recs);
   if (tiebreak && field_bits <= 64) {
     // one radix sort on the tag fields, then the query-name order inside runs of equal fields
     RoundKey rk{};
@@ -924,7 +926,8 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
     int th = (field_bits + kRadixBits - 1) / kRadixBits * kRadixBits - field_bits;  // free bits of the last digit
     if (th > tie_top) th = tie_top;
     if (field_bits + th > 64) th = 64 - field_bits;
-    LAUNCH_N("tag_keys", n, k_field_keys, grid, dim3(kBlock), s, *in, n, rk, tiebreak, tie_top, th, B.ka, B.va);
+    LAUNCH_N("tag_pack_keys", n, k_pack_field_keys, grid, dim3(kBlock), s, *in, n, rk, tiebreak, tie_top, th, recs,
+             B.ka, B.va);
     int which = 0;
     rc = radix_sort(B, n, field_bits + th, &which, s);
     if (rc) return rc;

@@ -287,13 +287,32 @@ __global__ void __launch_bounds__(kBlock) k_level1_plan(const int32_t* __restric
       const int q = (j0 + u) * kBlock + t;
       v[u] = (uint32_t)k1col[base + (q < tile_n ? q : 0)];
     }
+    // round 4: a wave whose positions in this batch lie in one run (the common case: runs are cells
+    // of thousands of records) takes that run's slot once, not per record (as the key pass does)
+    const int wo = t & ~(kWave - 1);
+    const int lo = j0 * kBlock + wo, hi = (j0 + kRunBatch - 1) * kBlock + wo + kWave - 1;
+    int ku = -2;  // the wave's uniform slot (-1: none), or -2: per record
+    if (hi < tile_n) {
+      const uint32_t llo = loc_of(lo, s_hb, s_wpre), lhi = loc_of(hi, s_hb, s_wpre);
+      if (__builtin_amdgcn_readfirstlane((int)llo) == __builtin_amdgcn_readfirstlane((int)lhi))
+        ku = slot_of(__builtin_amdgcn_readfirstlane((int)llo), sl);
+    }
+    if (ku >= 0) {
+      uint32_t* h = &s_h[ku * kRadix];
 #pragma unroll
-    for (int u = 0; u < kRunBatch; u++) {
-      const int q = (j0 + u) * kBlock + t;
-      if (q >= tile_n) continue;
-      const uint32_t k1 = v[u] < n_k1 ? v[u] : 0u;  // the key pass's rule for an invalid id
-      const int k = slot_of(loc_of(q, s_hb, s_wpre), sl);
-      if (k >= 0) atomicAdd(&s_h[k * kRadix + (b.scramble(k1) >> dshift)], 1u);
+      for (int u = 0; u < kRunBatch; u++) {
+        const uint32_t k1 = v[u] < n_k1 ? v[u] : 0u;  // the key pass's rule for an invalid id
+        atomicAdd(&h[b.scramble(k1) >> dshift], 1u);
+      }
+    } else if (ku == -2) {
+#pragma unroll
+      for (int u = 0; u < kRunBatch; u++) {
+        const int q = (j0 + u) * kBlock + t;
+        if (q >= tile_n) continue;
+        const uint32_t k1 = v[u] < n_k1 ? v[u] : 0u;
+        const int k = slot_of(loc_of(q, s_hb, s_wpre), sl);
+        if (k >= 0) atomicAdd(&s_h[k * kRadix + (b.scramble(k1) >> dshift)], 1u);
+      }
     }
   }
   __syncthreads();

@@ -270,17 +270,27 @@ constexpr int kTieShort = 16;
 // (tie_bits wide): the bits the last radix digit has free past the fields cost no pass, and they
 // split most runs of equal fields (duplicates rarely share their query-name rank's top bits), so
 // the run fix-up gathers the full tiebreak for far fewer records.
-__global__ void __launch_bounds__(kBlock) k_field_keys(sct_records_t r, int64_t n, RoundKey rk,
-                                                       const int32_t* __restrict__ tie, int tie_bits, int th,
-                                                       uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+// ... written with the packed row, in one pass over the columns (round 4: k_pack and a separate key
+// pass read the key fields twice)
+__global__ void __launch_bounds__(kBlock) k_pack_field_keys(sct_records_t r, int64_t n, RoundKey rk,
+                                                            const int32_t* __restrict__ tie, int tie_bits, int th,
+                                                            uint4* __restrict__ rows, uint64_t* __restrict__ keys,
+                                                            uint32_t* __restrict__ vals) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
   const uint32_t f[3] = {(uint32_t)r.cell[j], (uint32_t)r.umi[j], (uint32_t)r.gene[j]};
+  const uint4 a = make_uint4(f[0], f[1], f[2], (uint32_t)r.ref[j]);
+  const uint4 b = make_uint4((uint32_t)r.pos[j], (uint32_t)r.gq_sum[j] | ((uint32_t)r.gq_len[j] << 16),
+                             (uint32_t)r.gq_gt30[j] | ((uint32_t)r.bits[j] << 16) | ((uint32_t)r.xf[j] << 24),
+                             (uint32_t)r.cy_gt30[j] | ((uint32_t)r.cy_len[j] << 8) | ((uint32_t)r.uy_gt30[j] << 16) |
+                                 ((uint32_t)r.uy_len[j] << 24));
+  rows[2 * j] = a;
+  rows[2 * j + 1] = b;
   uint64_t k = 0;
   for (int i = 0; i < rk.nf; i++) {
-    const int b = rk.f[i].bits;
-    const uint64_t v = (uint64_t)f[rk.f[i].which] & (b >= 32 ? 0xFFFFFFFFull : ((1ull << b) - 1));
-    k = b ? ((b >= 64 ? 0ull : (k << b)) | v) : k;
+    const int bb = rk.f[i].bits;
+    const uint64_t v = (uint64_t)f[rk.f[i].which] & (bb >= 32 ? 0xFFFFFFFFull : ((1ull << bb) - 1));
+    k = bb ? ((bb >= 64 ? 0ull : (k << bb)) | v) : k;
   }
   if (th > 0) k = (k << th) | (((uint32_t)tie[j] >> (tie_bits - th)) & ((1u << th) - 1));
   keys[j] = k;
