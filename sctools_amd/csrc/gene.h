@@ -28,15 +28,16 @@ namespace sct {
 #define SCT_GENE_CHUNK 16384
 #endif
 constexpr int kGeneChunk = SCT_GENE_CHUNK;
-// Round 4: a bucket of >= kGeneHotBucket payloads (the Zipf head: ~55 % of the records in one
-// bucket at config 2) is reduced in items of kGeneChunkHot payloads -- each item ends with up to
-// kGenesPerBucket x 39 global atomics on the same 64 gene rows, so fewer, larger items cut that
-// write traffic; other buckets keep kGeneChunk (load balance)
+// Round 4: a bucket of >= kGeneHotBucket payloads (the Zipf head holds ~55 % of the records in one
+// bucket at config 2, the other buckets ~100k each) is reduced in items of kGeneChunkHot payloads:
+// each item ends with up to kGenesPerBucket x 39 global atomics on its bucket's 64 gene rows, so
+// fewer, larger items cut that write traffic (PMC writes 115 MB -> 63 MB with 64K items for the
+// head bucket alone); smaller buckets keep kGeneChunk
 #ifndef SCT_GENE_CHUNK_HOT
 #define SCT_GENE_CHUNK_HOT 65536
 #endif
 constexpr int kGeneChunkHot = SCT_GENE_CHUNK_HOT;
-constexpr uint64_t kGeneHotBucket = 16ull * kGeneChunkHot;
+constexpr uint64_t kGeneHotBucket = kGeneChunkHot;
 __device__ __forceinline__ uint64_t gene_chunk(uint64_t c) { return c >= kGeneHotBucket ? kGeneChunkHot : kGeneChunk; }
 constexpr int kGeneSub = 2048;  // 16-byte payloads sorted in LDS at a time (32 KB)
 constexpr int kGeneCnt = 1 + kGeneFlags;  // n_reads + flag counts (32-bit bins)

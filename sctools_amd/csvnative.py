@@ -81,7 +81,9 @@ def format_rows(names: Sequence[str], kinds: Sequence[int], slots: Sequence[int]
     return _take(out, n.value)
 
 
-def gzip(data: bytes, level: int = 9, chunk: int = 1 << 22, threads: int = 0) -> bytes:
+def gzip(data: bytes, level: int = 9, chunk: int = 1 << 18, threads: int = 0) -> bytes:
+    """gzip members of `chunk` input bytes compressed in parallel (concatenated members are one
+    valid gzip stream); 256 KB members spread even a few-thousand-row CSV over the cores."""
     L = load()
     out, n = ctypes.c_void_p(), ctypes.c_int64()
     if L.sct_csv_gzip(data, len(data), int(level), int(chunk), int(threads), ctypes.byref(out), ctypes.byref(n)):
