@@ -371,44 +371,15 @@ struct WelfordSide {
   }
 };
 
-// The chains' samples x = RN(a / b) of every record (k_welford_x).  Round 4: launched first, on the
-// caller's stream, before the entity count: on the side stream it ran beside the key pass and the
-// partition at a fraction of the device (1.4 ms of a 15 ms drop-in call, the chains waiting for it,
-// profiles/r04/g_welford_timeline/).  SCT_WF_XFIRST=0 keeps it on the side stream.
-bool welford_x_first() {
-  static const char* e = getenv("SCT_WF_XFIRST");
-  return !(e && e[0] == '0');
-}
-int launch_welford_x(const Layout& L, void* ws, bool cell, int64_t n, const RecCols& rc2, hipStream_t st) {
-  double* xs = at<double>(ws, L.wx);
-  const dim3 xgrid((unsigned)cdiv(n, kBlock));
-  if (cell) {
-    LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), st, rc2, n, xs);
-  } else {
-    LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), st, rc2, n, xs);
-  }
-  return SCT_OK;
-}
-
 int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent, const RecCols& rc2,
-                  const int64_t* ent_start, double* out_f, hipStream_t s, WelfordSide& wf, bool x_done) {
+                  const int64_t* ent_start, double* out_f, hipStream_t s, WelfordSide& wf) {
   // the side stream lives on the caller's stream's device (the calling thread's current device
   // may be another one)
   int dev = 0, prev = 0;
   HIPCHK(hipStreamGetDevice(s, &dev));
   HIPCHK(hipGetDevice(&prev));
   if (prev != dev) HIPCHK(hipSetDevice(dev));
-  // SCT_WF_PRIO=1: the side stream at the device's highest priority (its blocks dispatched ahead
-  // of the partition's)
-  static const char* prio_env = getenv("SCT_WF_PRIO");
-  hipError_t ce;
-  if (prio_env && prio_env[0] == '1') {
-    int lo = 0, hi = 0;
-    ce = hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if (ce == hipSuccess) ce = hipStreamCreateWithPriority(&wf.s2, hipStreamNonBlocking, hi);
-  } else {
-    ce = hipStreamCreateWithFlags(&wf.s2, hipStreamNonBlocking);
-  }
+  hipError_t ce = hipStreamCreateWithFlags(&wf.s2, hipStreamNonBlocking);
   if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.fork, hipEventDisableTiming);
   if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.join, hipEventDisableTiming);
   if (prev != dev) HIPCHK(hipSetDevice(prev));
@@ -424,14 +395,13 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
     LAUNCH("welford_bins", k_welford_bins, egrid, dim3(kBlock), s2, ent_start, n_ent, n, wc);
     LAUNCH("welford_order", k_welford_order, egrid, dim3(kBlock), s2, ent_start, n_ent, n, wc, worder);
     double* xs = at<double>(ws, L.wx);
-    if (!x_done) {
-      const int rx = launch_welford_x(L, ws, cell, n, rc2, s2);
-      if (rx) return rx;
-    }
+    const dim3 xgrid((unsigned)cdiv(n, kBlock));
     if (cell) {
+      LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s2, rc2, n, xs);
       LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s2, ent_start, n_ent, n,
                (const uint32_t*)worder, wc, (const double*)xs, out_f);
     } else {
+      LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s2, rc2, n, xs);
       LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfBlocks), dim3(kBlock), s2, ent_start, n_ent, n,
                (const uint32_t*)worder, wc, (const double*)xs, out_f);
     }
@@ -455,13 +425,6 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   const bool exact = plan->float_mode == SCT_FLOAT_EXACT_SUM;
   const int32_t* ent_col = cell ? rec->cell : rec->gene;
 
-  const bool x_first = !exact && out_i && n >= kWfWave && welford_x_first();
-  if (x_first) {
-    const RecCols rx{rec->ref, rec->pos, rec->gq_sum, rec->gq_len, rec->gq_gt30, rec->bits, rec->xf,
-                     rec->cy_gt30, rec->cy_len, rec->uy_gt30, rec->uy_len};
-    const int r0 = launch_welford_x(L, ws, cell, n, rx, s);
-    if (r0) return r0;
-  }
   int64_t n_ent = 0;
   bool dup = false;
   int rc = count_runs(ent_col, n, ws, L, gene, plan->n_cell_ids, &n_ent, &dup, s);
@@ -541,15 +504,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     rc = bucket_level1_plan(L, ws, kc, n, n_ent, b, ent_start, l1, s);
     if (rc) return rc;
   }
-  // SCT_WF_EARLY=1: the Welford stage forks as soon as the entity starts exist (after the level-1
-  // plan), before the key pass, so its long chains start before the partition fills the device
-  static const char* early_env = getenv("SCT_WF_EARLY");
-  const bool wf_early = planned && early_env && early_env[0] == '1';
-  WelfordSide wf;
-  if (wf_early && !exact && out_i) {
-    rc = welford_stage(L, ws, cell, n, n_ent, rc2, ent_start, out_f, s, wf, x_first);
-    if (rc) return rc;
-  }
+
   // gene payload format: narrow (8 B) unless an operand does not fit (checked by the exact-stream
   // pass; without it the wide format is used)
   uint32_t* gwide = reinterpret_cast<uint32_t*>(at<uint64_t>(ws, L.scalars) + 16);
@@ -573,8 +528,9 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     if (err & 2) return fail(SCT_EINVAL, "a gene / cell / umi id lies outside its dictionary size");
   }
   if (rc) return rc;
-  if (!wf_early && !exact && out_i) {  // the entity starts exist now (k_level1_plan or the key pass)
-    rc = welford_stage(L, ws, cell, n, n_ent, rc2, ent_start, out_f, s, wf, x_first);
+  WelfordSide wf;
+  if (!exact && out_i) {  // the entity starts exist now (k_level1_plan or the key pass)
+    rc = welford_stage(L, ws, cell, n, n_ent, rc2, ent_start, out_f, s, wf);
     if (rc) return rc;
   }
 
