@@ -175,6 +175,61 @@ __global__ void __launch_bounds__(kBlock) k_welford_x(RecCols r, int64_t n, doub
   o[1] = make_double2(x[2], kCell ? x[3] : 0.0);
 }
 
+// Round 4: the head groups (the kWfHeadGroups x kWfGroup largest entities: the longest chains decide
+// the drop-in's time) get their samples first and their chains launched at once; the rest follows
+// on another stream.  k_welford_split gives the head groups their own queue (ctl_head) and starts
+// the main queue after them; k_welford_x_ents computes the samples of the head entities' records
+// only (a grid-stride loop over their concatenation).
+constexpr int kWfHeadGroups = 4;
+constexpr int kWfHeadEnts = kWfHeadGroups * (kWave / 4);
+__global__ void k_welford_split(WelfordCtl* __restrict__ ctl, WelfordCtl* __restrict__ ctl_head) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t nb = ctl->n_big;
+  ctl_head->n_big = nb < (uint32_t)kWfHeadEnts ? nb : (uint32_t)kWfHeadEnts;
+  ctl_head->head = 0;
+  ctl->head = kWfHeadGroups;  // the first kWfHeadGroups groups are the head queue's
+}
+template <bool kCell>
+__global__ void __launch_bounds__(kBlock) k_welford_x_ents(RecCols r, const int64_t* __restrict__ ent_start,
+                                                           int64_t n_ent, int64_t n, const uint32_t* __restrict__ order,
+                                                           const WelfordCtl* __restrict__ ctl_head,
+                                                           double* __restrict__ xs) {
+  __shared__ double s_rcp[kRcpN];
+  __shared__ int64_t s_beg[kWfHeadEnts], s_pre[kWfHeadEnts + 1];
+  fill_rcp(s_rcp);
+  const int m = (int)ctl_head->n_big;  // <= kWfHeadEnts
+  if (threadIdx.x < kWfHeadEnts) {
+    int64_t b = 0, len = 0;
+    if ((int)threadIdx.x < m) {
+      const int64_t e = order[threadIdx.x];
+      b = ent_start[e];
+      len = ent_end(ent_start, e, n_ent, n) - b;
+    }
+    s_beg[threadIdx.x] = b;
+    s_pre[threadIdx.x + 1] = len;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s_pre[0] = 0;
+    for (int k = 1; k <= kWfHeadEnts; k++) s_pre[k] += s_pre[k - 1];
+  }
+  __syncthreads();
+  const int64_t total = s_pre[m];
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < total; j += (int64_t)gridDim.x * kBlock) {
+    int lo = 0, hi = m - 1;  // the entity k with s_pre[k] <= j < s_pre[k + 1]
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) / 2;
+      if (s_pre[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    const int64_t i = s_beg[lo] + (j - s_pre[lo]);
+    double x[4];
+    welford_samples<kCell>(r, i, s_rcp, x);
+    double2* o = reinterpret_cast<double2*>(xs + 4 * i);
+    o[0] = make_double2(x[0], x[1]);
+    o[1] = make_double2(x[2], kCell ? x[3] : 0.0);
+  }
+}
+
 // Big entities: one lane per (entity, stream) chain, kWfGroup entities x 4 streams per wave, groups
 // of similar sizes (the order is by descending log2 size), waves dequeue groups.  Every lane steps
 // the same record index k together, so RN(1 / k) is the same for all of them: the wave computes 64

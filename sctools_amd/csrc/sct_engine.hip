@@ -25,6 +25,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "comm.h"
 #include "common.h"
 #include "countmat.h"
@@ -112,7 +114,7 @@ Layout layout_for(const sct_plan_t* plan) {
   L.giants = take(sizeof(Seg) * (size_t)L.max_seg);
   L.bigs = take(sizeof(Seg) * (size_t)L.max_seg);
   const bool welford = plan->float_mode == SCT_FLOAT_WELFORD;
-  L.wctl = take(welford ? sizeof(WelfordCtl) : 0);
+  L.wctl = take(welford ? 2 * sizeof(WelfordCtl) : 0);  // the main queue and the head group's
   L.worder = take(welford ? sizeof(uint32_t) * (size_t)L.max_ent : 0);
   L.wx = take(welford ? sizeof(double) * 4 * (size_t)(n1 + kWfPad) : 0);  // every record's stream values
   L.total = off;
@@ -361,15 +363,37 @@ int launch_build_keys(bool cell, bool gene, dim3 grid, hipStream_t s, const KeyC
 // only the mean / variance slots of the output rows (k_finalize writes the others), so it runs on a
 // side stream from the moment the entity starts exist, beside the key pass' successors (bucket
 // partition, hash tiles) on the caller's stream.
+// The two side streams are created once per device and process (round 4: creating them per call
+// cost ~0.6 ms of host time before the first Welford launch); concurrent pipelines on one device
+// share them (their kernels then queue behind each other; every call waits on its own events).
 struct WelfordSide {
-  hipStream_t s2 = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  ~WelfordSide() {  // the caller's stream waits on `join` before anything after the pipeline runs
+  hipStream_t s2 = nullptr, s3 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, fork3 = nullptr, join3 = nullptr;
+  ~WelfordSide() {  // the caller's stream waits on `join` and `join3` before anything after the pipeline
     if (fork) (void)hipEventDestroy(fork);
     if (join) (void)hipEventDestroy(join);
-    if (s2) (void)hipStreamDestroy(s2);
+    if (fork3) (void)hipEventDestroy(fork3);
+    if (join3) (void)hipEventDestroy(join3);
   }
 };
+constexpr int kMaxSideDevices = 64;
+hipError_t side_streams(int dev, hipStream_t* s2, hipStream_t* s3) {
+  static std::mutex mu;
+  static hipStream_t ss[kMaxSideDevices][2] = {};
+  if (dev < 0 || dev >= kMaxSideDevices) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> g(mu);
+  for (int i = 0; i < 2; i++)
+    if (!ss[dev][i]) {
+      const hipError_t e = hipStreamCreateWithFlags(&ss[dev][i], hipStreamNonBlocking);
+      if (e != hipSuccess) {
+        ss[dev][i] = nullptr;
+        return e;
+      }
+    }
+  *s2 = ss[dev][0];
+  *s3 = ss[dev][1];
+  return hipSuccess;
+}
 
 int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent, const RecCols& rc2,
                   const int64_t* ent_start, double* out_f, hipStream_t s, WelfordSide& wf) {
@@ -379,37 +403,56 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
   HIPCHK(hipStreamGetDevice(s, &dev));
   HIPCHK(hipGetDevice(&prev));
   if (prev != dev) HIPCHK(hipSetDevice(dev));
-  hipError_t ce = hipStreamCreateWithFlags(&wf.s2, hipStreamNonBlocking);
+  hipError_t ce = side_streams(dev, &wf.s2, &wf.s3);
   if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.fork, hipEventDisableTiming);
   if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.join, hipEventDisableTiming);
+  if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.fork3, hipEventDisableTiming);
+  if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.join3, hipEventDisableTiming);
   if (prev != dev) HIPCHK(hipSetDevice(prev));
   HIPCHK(ce);
   HIPCHK(hipEventRecord(wf.fork, s));
   HIPCHK(hipStreamWaitEvent(wf.s2, wf.fork, 0));
-  hipStream_t s2 = wf.s2;
+  hipStream_t s2 = wf.s2, s3 = wf.s3;
   const dim3 egrid((unsigned)cdiv(n_ent, kBlock));
   if (n >= kWfWave) {
     WelfordCtl* wc = at<WelfordCtl>(ws, L.wctl);
+    WelfordCtl* wch = wc + 1;  // the head group's queue
     uint32_t* worder = at<uint32_t>(ws, L.worder);
-    HIPCHK(hipMemsetAsync(wc, 0, sizeof(WelfordCtl), s2));
+    HIPCHK(hipMemsetAsync(wc, 0, 2 * sizeof(WelfordCtl), s2));
     LAUNCH("welford_bins", k_welford_bins, egrid, dim3(kBlock), s2, ent_start, n_ent, n, wc);
     LAUNCH("welford_order", k_welford_order, egrid, dim3(kBlock), s2, ent_start, n_ent, n, wc, worder);
+    LAUNCH("welford_split", k_welford_split, dim3(1), dim3(kWave), s2, wc, wch);
+    // the rest on s3: every record's samples, then the other groups' chains and the small entities
+    HIPCHK(hipEventRecord(wf.fork3, s2));
+    HIPCHK(hipStreamWaitEvent(s3, wf.fork3, 0));
     double* xs = at<double>(ws, L.wx);
     const dim3 xgrid((unsigned)cdiv(n, kBlock));
+    const dim3 hgrid((unsigned)kWfBlocks);
     if (cell) {
-      LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s2, rc2, n, xs);
-      LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s2, ent_start, n_ent, n,
+      LAUNCH("welford_x_head", k_welford_x_ents<true>, hgrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n,
+             (const uint32_t*)worder, (const WelfordCtl*)wch, xs);
+      LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfHeadGroups), dim3(kBlock), s2, ent_start, n_ent, n,
+               (const uint32_t*)worder, wch, (const double*)xs, out_f);
+      LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s3, rc2, n, xs);
+      LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,
                (const uint32_t*)worder, wc, (const double*)xs, out_f);
     } else {
-      LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s2, rc2, n, xs);
-      LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfBlocks), dim3(kBlock), s2, ent_start, n_ent, n,
+      LAUNCH("welford_x_head", k_welford_x_ents<false>, hgrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n,
+             (const uint32_t*)worder, (const WelfordCtl*)wch, xs);
+      LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfHeadGroups), dim3(kBlock), s2, ent_start, n_ent, n,
+               (const uint32_t*)worder, wch, (const double*)xs, out_f);
+      LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s3, rc2, n, xs);
+      LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,
                (const uint32_t*)worder, wc, (const double*)xs, out_f);
     }
+  } else {
+    HIPCHK(hipEventRecord(wf.fork3, s2));
+    HIPCHK(hipStreamWaitEvent(s3, wf.fork3, 0));
   }
   if (cell) {
-    LAUNCH("welford", k_welford<true>, egrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n, out_f);
+    LAUNCH("welford", k_welford<true>, egrid, dim3(kBlock), s3, rc2, ent_start, n_ent, n, out_f);
   } else {
-    LAUNCH("welford", k_welford<false>, egrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n, out_f);
+    LAUNCH("welford", k_welford<false>, egrid, dim3(kBlock), s3, rc2, ent_start, n_ent, n, out_f);
   }
   return SCT_OK;
 }
@@ -504,6 +547,15 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     rc = bucket_level1_plan(L, ws, kc, n, n_ent, b, ent_start, l1, s);
     if (rc) return rc;
   }
+  // Welford (the drop-in default): forked as soon as the entity starts exist -- after the level-1
+  // plan when there is one (round 4: the head group's chains then start before the key pass),
+  // else after the key pass
+  WelfordSide wf;
+  const bool wf_fork_early = planned && !exact && out_i;
+  if (wf_fork_early) {
+    rc = welford_stage(L, ws, cell, n, n_ent, rc2, ent_start, out_f, s, wf);
+    if (rc) return rc;
+  }
 
   // gene payload format: narrow (8 B) unless an operand does not fit (checked by the exact-stream
   // pass; without it the wide format is used)
@@ -528,8 +580,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     if (err & 2) return fail(SCT_EINVAL, "a gene / cell / umi id lies outside its dictionary size");
   }
   if (rc) return rc;
-  WelfordSide wf;
-  if (!exact && out_i) {  // the entity starts exist now (k_level1_plan or the key pass)
+  if (!wf_fork_early && !exact && out_i) {  // the entity starts exist now (the key pass wrote them)
     rc = welford_stage(L, ws, cell, n, n_ent, rc2, ent_start, out_f, s, wf);
     if (rc) return rc;
   }
@@ -540,6 +591,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     rc = bucket_distinct(L, ws, n, n_ent, ent_start, mito, b, cell, gene, partials, dflags, planned, s);
     if (rc == 1) {  // a mapped ref id does not fit the bucket payload: redo on the global-sort path
       if (wf.s2) HIPCHK(hipStreamSynchronize(wf.s2));  // (its workspace is reused by the redo)
+      if (wf.s3) HIPCHK(hipStreamSynchronize(wf.s3));
       return pipeline(plan, rec, gene_is_mito, ws, ws_bytes, out_i, out_f, capacity, n_rows, gene_partials, s,
                       false);
     }
@@ -566,9 +618,11 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   if (out_i) {
     LAUNCH("finalize", k_finalize, dim3((unsigned)cdiv(n_ent * kFinThreads, kBlock)), dim3(kBlock), s, (const int64_t*)partials,
            n_ent, cell ? SCT_MODE_CELL : SCT_MODE_GENE, exact ? 1 : 0, (const int64_t*)ent_start, out_i, out_f);
-    if (!exact) {  // launched on the side stream after the key pass (welford_stage): joined here
+    if (!exact) {  // launched on the side streams after the key pass (welford_stage): joined here
       HIPCHK(hipEventRecord(wf.join, wf.s2));
       HIPCHK(hipStreamWaitEvent(s, wf.join, 0));
+      HIPCHK(hipEventRecord(wf.join3, wf.s3));
+      HIPCHK(hipStreamWaitEvent(s, wf.join3, 0));
     }
   }
   if (gene) {
