@@ -125,7 +125,7 @@ def parse():
                     help="config 5: the order sorted inside every step -- (CB, UB, GE) then query name, as "
                          "bam.sort_by_tags_and_queryname (bam.py:698-709) / TagSortBam define it (default), "
                          "or CB only (all the cell and grouped gene metrics need)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json"),
                     help="rocprofv3 --pmc per-kernel HBM bytes (tools/pmc_passes.sh) for roofline.traffic")
     return ap.parse_args()
 
