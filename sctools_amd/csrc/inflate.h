@@ -30,9 +30,10 @@ constexpr uint32_t kLitBits = 10, kDistBits = 8, kClBits = 7;
 // The LDS window holds the newest kWin output bytes; older ones are read back from the member's
 // output in HBM, already flushed there (pos - flushed <= kFlush + 258 < kWin at every copy), so a
 // smaller window costs only those far matches and buys waves per CU (24M-record BAM: inflate
-// 0.459 s with a 32 KB window at 4 waves per CU, 0.347 s at 16 KB, 0.246 s at 8 KB, 0.180 s at 4 KB).
+// 0.459 s with a 32 KB window at 4 waves per CU, 0.347 s at 16 KB, 0.246 s at 8 KB, 0.180 s at 4 KB;
+// round 4, 20M-record config-2-shaped BAM: 0.147 s at 4 KB, 0.139 s at 2 KB, profiles/r04/h_inflate_window/).
 #ifndef SCT_INFL_WIN
-#define SCT_INFL_WIN 4096
+#define SCT_INFL_WIN 2048
 #endif
 constexpr uint32_t kWin = SCT_INFL_WIN, kWinMask = kWin - 1, kFlush = kWin / 4;
 static_assert((kWin & (kWin - 1)) == 0 && kWin >= 2048 && kWin <= 32768, "a power-of-two window");
