@@ -28,8 +28,9 @@ namespace gb {
 
 // (round 4: a 9-bit literal / length root table -- 2 KB of LDS instead of 4 KB, so 20 waves per CU
 // instead of 17; longer codes take the slow path: inflate 0.141 -> 0.122 s on a 20M-record
-// config-2-shaped BAM, profiles/r04/h_inflate_window/)
-constexpr uint32_t kLitBits = 9, kDistBits = 8, kClBits = 7;
+// config-2-shaped BAM; then an 8-bit one, 1 KB: 0.122 -> 0.112 s; a 7-bit distance table gained
+// nothing (0.123 s); profiles/r04/h_inflate_window/)
+constexpr uint32_t kLitBits = 8, kDistBits = 8, kClBits = 7;
 // The LDS window holds the newest kWin output bytes; older ones are read back from the member's
 // output in HBM, already flushed there (pos - flushed <= kFlush + 258 < kWin at every copy), so a
 // smaller window costs only those far matches and buys waves per CU (24M-record BAM: inflate
