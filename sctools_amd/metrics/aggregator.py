@@ -84,7 +84,13 @@ class MetricAggregator:
     # ---- aggregator protocol (aggregator.py:236-340) ----
     def parse_molecule(self, tags: Sequence[str], records) -> None:
         """aggregator.py:251-334, record by record: the subclass fields first, then the counters,
-        raising where the reference raises."""
+        raising where the reference raises.
+
+        Known gap: a record that raises part-way (a mapped read without an XF or NH tag, a record
+        past the 32-byte columnar limits) is not buffered.  The reference has by then already
+        counted it in n_reads, the molecule and fragment histograms and the quality streams, so a
+        caller that catches the error and still calls finalize() gets those metrics without that
+        record (finalize() recomputes every column from the buffered records)."""
         for record in records:
             self._extra = (0, 0)
             self.parse_extra_fields(tags=tags, record=record)
