@@ -1,0 +1,7 @@
+import sys
+p = sys.argv[1] + "/finalize.h"
+s = open(p).read()
+old = "            for (int q = 0; q < kWfBatch; q++) xn[q] = B[4 * q];"
+assert old in s
+s = s.replace(old, "            for (int q = 0; q < kWfBatch; q++) xn[q] = (double)((q * 7 + (int)c) & 15) * 0.0625 + (double)(B == xs);")
+open(p, "w").write(s)
