@@ -170,25 +170,34 @@ def main():
         cfg.p_nh1, cfg.p_dup, cfg.p_secondary = 0.70, 0.40, 0.10
     data = synth.generate(cfg, device=dev, chunk=16_000_000)
     qname, n_qnames = None, 0
+    n_cell_ids = data.n_cell_ids
     if args.config == 5:  # global permutation: the step must regroup records itself
         g = torch.Generator(device=dev)
         g.manual_seed(args.seed + 1 + 1000 * rank)
         perm = torch.randperm(args.records, generator=g, device=dev)
         data.cols = {c: t[perm].contiguous() for c, t in data.cols.items()}
         qname, n_qnames = data.extra["qname"][perm].contiguous(), data.extra["n_qnames"]
-        data.extra["qname"] = qname
         del perm
+        if world > 1:
+            qname, n_qnames, n_cell_ids = deal_records(data, qname, n_qnames, world, rank, dev, args.seed)
+        data.extra["qname"] = qname
     torch.cuda.synchronize()
     if rank == 0:
         log("generated %d records/rank in %.1fs" % (args.records, time.time() - t0))
-    dims = E.Dims(data.n_cell_ids, data.n_gene_ids, data.n_umi_ids)
+    dims = E.Dims(n_cell_ids, data.n_gene_ids, data.n_umi_ids)
     mito = torch.from_numpy(data.gene_is_mito).to(dev)
     multi = torch.from_numpy(data.gene_is_multi).to(dev)
     def regroup(cols):
-        """config 5: TagSortBam's order on the GPU (the step's first stage)."""
+        """config 5: TagSortBam's order on the GPU (the step's first stage); at N > 1 first the cell
+        bins swapped between ranks (SplitBam's bins, bam.py:439-480): each rank then sorts its cells."""
+        tie = qname
+        if world > 1:
+            binned, btie, counts = eng.bin_records(cols, dims, world, qname if args.sort_order != "cell" else None)
+            cols, tie, _ = D.exchange_records(binned, btie, counts)
+            del binned, btie
         if args.sort_order == "cell":
             return eng.tag_sort(cols, dims, "cell")
-        return eng.tag_sort(cols, dims, "cell_umi_gene", qname, n_qnames)
+        return eng.tag_sort(cols, dims, "cell_umi_gene", tie, n_qnames)
 
     if args.config == 5:
         n_ent = eng.count_entities(regroup(data.cols), "cell", dims)
@@ -252,14 +261,20 @@ def main():
     prof = eng.profile_read_items()
     elapsed = t1 - t0
     allreduce_ms = time_allreduce(partials, dev) if world > 1 else None
-    side = side_measurements(eng, data, dims, mito, multi, args, regroup) if rank == 0 else {}
+    step_cols = regroup(data.cols) if args.config == 5 else data.cols  # (every rank: a collective at N > 1)
+    side = side_measurements(eng, data, dims, mito, multi, args, step_cols) if rank == 0 else {}
+    del step_cols
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # sanity: every record accounted on both sides
+    # sanity: every record accounted on both sides (config 5 at N > 1: each rank's cells after the swap)
     n_cell_reads = int(host_cells[:rows, 0].sum())
+    if world > 1 and args.config == 5:
+        t = torch.tensor([n_cell_reads], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        n_cell_reads = int(t.item()) // world
     if not args.no_check:
         assert n_cell_reads == args.records, (n_cell_reads, args.records)
         assert int(host_genei[:, 0].sum()) == args.records * world
@@ -327,7 +342,9 @@ def main():
                 "workload": ({2: "config2: %d cell-sorted records/rank",
                               4: "config4: %d cell-sorted records/rank, lognormal(0, 2) reads per cell",
                               5: "config5: %d globally shuffled records/rank (30%% NH>1, 40%% dup, secondary alignments), "
-                                 "GPU sort by " + ("(CB, UB, GE, query name)" if args.sort_order != "cell" else "CB")}
+                                 + ("records of every rank's cells dealt to every rank, cell bins swapped over RCCL "
+                                    "each step, then " if world > 1 else "")
+                                 + "GPU sort by " + ("(CB, UB, GE, query name)" if args.sort_order != "cell" else "CB")}
                              [args.config]) % args.records + ", %d cells/rank, %d genes; cell metrics + grouped gene metrics%s"
                             % (args.cells, args.genes, " + RCCL all-reduce" if world > 1 else ""),
                 "records_per_rank": args.records,
@@ -355,7 +372,33 @@ def main():
         dist.destroy_process_group()
 
 
-def side_measurements(eng, data, dims, mito, multi, args, regroup):
+def deal_records(data, qname, n_qnames, world, rank, dev, seed):
+    """config 5 at N > 1 (setup, untimed): one globally shuffled record set over the ranks.  Each
+    rank's generated cells get global ids (rank r's cells follow rank r - 1's) and its query-name
+    ranks a global offset; its shuffled records are cut into `world` equal pieces and piece q goes
+    to rank q (all_to_all), and every rank shuffles what it received.  So every rank holds records
+    of every rank's cells in no order, and each step must swap the cell bins before it can sort.
+    Returns (qname, total query names, global cell ids)."""
+    from sctools_amd import distributed as D
+
+    n = data.cols["cell"].numel()
+    nq = torch.tensor([n_qnames], dtype=torch.int64, device=dev)
+    all_nq = [torch.zeros_like(nq) for _ in range(world)]
+    dist.all_gather(all_nq, nq)
+    all_nq = [int(x.item()) for x in all_nq]
+    data.cols["cell"] = data.cols["cell"] + rank * data.n_cell_ids  # (every rank: the same cell count)
+    qname = qname + int(sum(all_nq[:rank]))
+    piece = torch.tensor([n * (q + 1) // world - n * q // world for q in range(world)], dtype=torch.int64,
+                         device=dev)
+    cols, qname, _ = D.exchange_records(data.cols, qname, piece)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed + 7 + 1000 * rank)
+    perm = torch.randperm(cols["cell"].numel(), generator=g, device=dev)
+    data.cols = {c: t[perm].contiguous() for c, t in cols.items()}
+    return qname[perm].contiguous(), int(sum(all_nq)), data.n_cell_ids * world
+
+
+def side_measurements(eng, data, dims, mito, multi, args, cols):
     """Costs kept OUT of `value`, reported beside it:
     * the H2D copy of the 32-B SoA columns from pinned host memory (the bench generates its
       shard in HBM; a caller handing over host buffers pays this once per shard);
@@ -382,7 +425,6 @@ def side_measurements(eng, data, dims, mito, multi, args, regroup):
     del dst, pinned
     out["h2d"] = {"ms": h2d_s * 1e3, "bytes": nbytes, "GB_per_s": nbytes / h2d_s / 1e9,
                   "note": "pinned host -> HBM copy of the SoA columns; excluded from value"}
-    cols = data.cols if args.config != 5 else regroup(data.cols)
     eng.count_entities(cols, "cell", dims)
     torch.cuda.synchronize()
     t0 = time.perf_counter()

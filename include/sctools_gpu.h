@@ -269,6 +269,48 @@ int sct_verify_sort(const sct_plan_t* plan, const sct_records_t* rec, const int3
                     int32_t order, void* workspace, size_t workspace_bytes,
                     int64_t* first_violation /* host */, void* stream);
 
+/* ---- multi-GPU for unsorted input: cell bins exchanged between devices ----
+ * The reference's route for an unsorted BAM: SplitBam gives every cell barcode a bin
+ * (bam.py:439-448), writes each input's records to their bins (write_barcodes_to_bins,
+ * bam.py:454-463) and merges each bin's pieces (bam.py:465-480); every chunk is then sorted
+ * (TagSortBam, platform.py:55-97) and measured.  Here each device bins its part of the records
+ * (sct_bin_records), the devices swap bins over RCCL (sct_exchange_counts, then
+ * sct_exchange_records: bin r of every rank to rank r, in rank order), and each device sorts
+ * and measures its cells (sct_tag_sort, sct_cell_metrics_gene_partials), the gene partials
+ * summed by sct_allreduce_gene_partials.  Bins keep input order, so a rank whose parts are
+ * consecutive file ranges receives its cells' records in file order. */
+#define SCT_MAX_BINS 256
+
+/* Device workspace bytes for sct_bin_records of plan->n_records records into n_bins bins. */
+int sct_bin_workspace_size(const sct_plan_t* plan, int32_t n_bins, size_t* bytes);
+
+/* Stable partition of `in` into `out` (caller-allocated device columns of n records; must not
+ * alias `in`) by the bin of each record's cell: bin_of_cell[cell] (device uint8 per cell id,
+ * values >= n_bins go to the last bin), or, when bin_of_cell is NULL, contiguous id ranges
+ * cell * n_bins / n_cell_ids (ids are ranks of the sorted barcodes, so bins follow barcode
+ * order).  Bin 0's records first; input order kept inside a bin.  `tiebreak` (nullable device
+ * int32) is carried along into `tiebreak_out`.  bin_counts: device int64[n_bins], written.
+ * 1 <= n_bins <= SCT_MAX_BINS.  Does not synchronize `stream`. */
+int sct_bin_records(const sct_plan_t* plan, const sct_records_t* in, const int32_t* tiebreak,
+                    const uint8_t* bin_of_cell, int32_t n_bins, const sct_records_t* out,
+                    int32_t* tiebreak_out, int64_t* bin_counts, void* workspace, size_t workspace_bytes,
+                    void* stream);
+
+/* Every rank's bin counts swapped: recv_counts[p] (device int64[n_ranks]) = send_counts[me] of
+ * rank p (device int64[n_ranks], this rank's bin sizes).  n_ranks = the communicator's size. */
+int sct_exchange_counts(const int64_t* send_counts, int64_t* recv_counts, int32_t n_ranks, void* comm,
+                        void* stream);
+
+/* The binned records swapped: bin p of this rank (send_counts[p] records from the start of
+ * bin p in `binned`) goes to rank p; `out` (out->n = sum(recv_counts)) receives rank 0's
+ * piece first, then rank 1's, ... .  send_counts / recv_counts are HOST int64[n_ranks]
+ * (sct_exchange_counts' result, copied back).  `tiebreak` / `tiebreak_out`: an optional int32
+ * column exchanged alongside (both or neither).  One RCCL group of send/recv pairs per peer
+ * and column; this rank's own bin is a device copy.  Does not synchronize `stream`. */
+int sct_exchange_records(const sct_records_t* binned, const int32_t* tiebreak, const int64_t* send_counts,
+                         const int64_t* recv_counts, int32_t n_ranks, const sct_records_t* out,
+                         int32_t* tiebreak_out, void* comm, void* stream);
+
 /* ---- count matrix (CountMatrix.from_sorted_tagged_bam, count.py:134-328) ---- */
 
 #define SCT_COUNT_SKIP (-1)    /* gene_col: never counted (missing tag, or a multi-gene "a,b" value) */

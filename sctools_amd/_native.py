@@ -38,7 +38,9 @@ EXPORTED = ("sct_abi_version", "sct_last_error", "sct_workspace_size", "sct_coun
             "sct_profile_read_items",
             "sct_tag_sort_workspace_size", "sct_tag_sort", "sct_verify_sort", "sct_count_matrix_workspace_size", "sct_count_matrix",
             "sct_allreduce_gene_partials", "sct_comm_unique_id", "sct_comm_init_rank", "sct_comm_init_all",
-            "sct_comm_destroy", "sct_comm_abort")
+            "sct_comm_destroy", "sct_comm_abort", "sct_bin_workspace_size", "sct_bin_records", "sct_exchange_counts",
+            "sct_exchange_records")
+SCT_MAX_BINS = 256
 ORDER_CELL, ORDER_CELL_UMI_GENE, ORDER_GENE_CELL_UMI = 0, 1, 2
 PLAN_GENE_PARTIALS = 0x1
 
@@ -157,6 +159,17 @@ def load() -> ctypes.CDLL:
     if hasattr(L, "sct_comm_abort"):
         L.sct_comm_abort.restype = ctypes.c_int
         L.sct_comm_abort.argtypes = [vp]
+    if hasattr(L, "sct_bin_records"):  # (an older engine given by SCT_LIB_PATH for an A/B lacks them)
+        L.sct_bin_workspace_size.restype = ctypes.c_int
+        L.sct_bin_workspace_size.argtypes = [ctypes.POINTER(Plan), i32, ctypes.POINTER(ctypes.c_size_t)]
+        L.sct_bin_records.restype = ctypes.c_int
+        L.sct_bin_records.argtypes = [ctypes.POINTER(Plan), ctypes.POINTER(Records), vp, vp, i32,
+                                      ctypes.POINTER(Records), vp, vp, vp, ctypes.c_size_t, vp]
+        L.sct_exchange_counts.restype = ctypes.c_int
+        L.sct_exchange_counts.argtypes = [vp, vp, i32, vp, vp]
+        L.sct_exchange_records.restype = ctypes.c_int
+        L.sct_exchange_records.argtypes = [ctypes.POINTER(Records), vp, ctypes.POINTER(i64), ctypes.POINTER(i64), i32,
+                                           ctypes.POINTER(Records), vp, vp, vp]
     L.sct_profile_enable.restype = ctypes.c_int
     L.sct_profile_enable.argtypes = [ctypes.c_int]
     L.sct_profile_only.restype = ctypes.c_int

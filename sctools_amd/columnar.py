@@ -247,9 +247,10 @@ def cut_runs(shards: List[Dict], key: str) -> List[Dict]:
         if n == 0:
             continue
         if prev is not None:
-            last = shards[prev][key][-1]
+            # host values: the two shards may live on different devices
+            last = int(shards[prev][key][-1].item())
             col = sh[key]
-            if bool((col[0] == last).item()):
+            if int(col[0].item()) == last:
                 diff = torch.nonzero(col != col[0])
                 k = int(diff[0, 0].item()) if diff.numel() else n
                 dst = shards[prev][key].device

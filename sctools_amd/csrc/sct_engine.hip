@@ -30,6 +30,7 @@
 #include "comm.h"
 #include "common.h"
 #include "countmat.h"
+#include "exchange.h"
 #include "finalize.h"
 #include "fixedpt.h"
 #include "bucket.h"
@@ -1032,6 +1033,61 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
     hi = lo;
   }
   LAUNCH_N("tag_unpack", n, k_unpack, grid, dim3(kBlock), s, (const uint4*)recs, perm, n, *out);
+  return SCT_OK;
+}
+
+// ---- cell bins for the exchange between devices (exchange.h; SplitBam's bins, bam.py:439-480) ----
+
+int sct_bin_workspace_size(const sct_plan_t* plan, int32_t n_bins, size_t* bytes) {
+  last_error().clear();
+  if (!plan || !bytes) return fail(SCT_EINVAL, "NULL argument");
+  if (n_bins < 1 || n_bins > SCT_MAX_BINS) return fail(SCT_EINVAL, "n_bins %d outside [1, %d]", n_bins, SCT_MAX_BINS);
+  const int64_t tiles = cdiv(plan->n_records > 0 ? plan->n_records : 1, kBinTile);
+  const int64_t m = (int64_t)n_bins * tiles;
+  *bytes = 2 * align_up(sizeof(uint32_t) * (size_t)m) + align_up(sizeof(uint64_t) * (size_t)(cdiv(m, kScanChunk) + 1));
+  return SCT_OK;
+}
+
+int sct_bin_records(const sct_plan_t* plan, const sct_records_t* in, const int32_t* tiebreak,
+                    const uint8_t* bin_of_cell, int32_t n_bins, const sct_records_t* out, int32_t* tiebreak_out,
+                    int64_t* bin_counts, void* workspace, size_t workspace_bytes, void* stream) {
+  last_error().clear();
+  int rc = check_sort_args(plan, in);
+  if (rc) return rc;
+  if (!out || out->n != in->n) return fail(SCT_EINVAL, "out must hold records.n records");
+  if (n_bins < 1 || n_bins > SCT_MAX_BINS) return fail(SCT_EINVAL, "n_bins %d outside [1, %d]", n_bins, SCT_MAX_BINS);
+  if (!bin_counts) return fail(SCT_EINVAL, "bin_counts is NULL");
+  if ((tiebreak == nullptr) != (tiebreak_out == nullptr))
+    return fail(SCT_EINVAL, "tiebreak and tiebreak_out: both or neither");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = in->n;
+  if (n == 0) {
+    HIPCHK(hipMemsetAsync(bin_counts, 0, sizeof(int64_t) * (size_t)n_bins, s));
+    return SCT_OK;
+  }
+  size_t need = 0;
+  rc = sct_bin_workspace_size(plan, n_bins, &need);
+  if (rc) return rc;
+  if (!workspace || workspace_bytes < need) return fail(SCT_ENOMEM, "workspace too small (%zu < %zu)", workspace_bytes, need);
+  const int64_t tiles = cdiv(n, kBinTile);
+  const int64_t m = (int64_t)n_bins * tiles;
+  uint32_t* counts = (uint32_t*)workspace;
+  uint32_t* offsets = (uint32_t*)((uint8_t*)workspace + align_up(sizeof(uint32_t) * (size_t)m));
+  uint64_t* sums = (uint64_t*)((uint8_t*)workspace + 2 * align_up(sizeof(uint32_t) * (size_t)m));
+  const uint32_t nb = (uint32_t)n_bins, nc = (uint32_t)plan->n_cell_ids;
+  const int bin_bits = bitlen((uint64_t)n_bins);  // bits of the bin values 0 .. n_bins - 1
+  LAUNCH_N("bin_hist", n, k_bin_hist, dim3((unsigned)tiles), dim3(kBlock), s, in->cell, n, bin_of_cell, nb, nc, tiles,
+           counts);
+  rc = scan_counts(counts, m, offsets, sums, s);
+  if (rc) return rc;
+  if (tiebreak) {
+    LAUNCH_N("bin_scatter", n, k_bin_scatter<true>, dim3((unsigned)tiles), dim3(kBlock), s, *in, tiebreak, *out,
+             tiebreak_out, n, bin_of_cell, nb, nc, bin_bits, tiles, (const uint32_t*)offsets);
+  } else {
+    LAUNCH_N("bin_scatter", n, k_bin_scatter<false>, dim3((unsigned)tiles), dim3(kBlock), s, *in, tiebreak, *out,
+             tiebreak_out, n, bin_of_cell, nb, nc, bin_bits, tiles, (const uint32_t*)offsets);
+  }
+  LAUNCH("bin_totals", k_bin_totals, dim3(1), dim3(kBlock), s, (const uint32_t*)offsets, tiles, nb, n, bin_counts);
   return SCT_OK;
 }
 

@@ -63,6 +63,51 @@ def allreduce_partials(partials: torch.Tensor, group=None) -> torch.Tensor:
     return partials
 
 
+def exchange_records(binned: dict, tiebreak: Optional[torch.Tensor], counts: torch.Tensor,
+                     group=None) -> Tuple[dict, Optional[torch.Tensor], List[int]]:
+    """The cell-bin swap between ranks (SplitBam's bins, bam.py:439-480, as a collective): bin p of
+    this rank's ``binned`` columns (``counts[p]`` records, bins consecutive in bin order, as
+    ``Engine.bin_records`` lays them out) goes to rank p; this rank receives rank 0's bin for it,
+    then rank 1's, ... -- file order when rank r holds the r-th part of the file.  One
+    all_to_all of the counts, then one per column (RCCL with the ``nccl`` backend, gloo on CPU).
+    Returns (columns, tiebreak or None, received counts per source rank)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if counts.numel() != world:
+        raise ValueError("%d bin counts for %d ranks" % (counts.numel(), world))
+    if world == 1:
+        return dict(binned), tiebreak, [int(counts[0].item())]
+    # gloo moves host tensors only: device columns travel through host memory there
+    host = dist.get_backend(group) == "gloo" and counts.device.type != "cpu"
+    dev = counts.device
+
+    def io(t):
+        return t.cpu() if host else t
+
+    send = io(counts.to(torch.int64))
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    send_l, recv_l = send.tolist(), recv.tolist()
+    total = int(sum(recv_l))
+
+    def swap(t):
+        src = io(t.contiguous())
+        dt = src.dtype
+        # 8- and 16-bit columns: gloo has no such all_to_all types (widened to int32 and back); RCCL
+        # moves 16-bit words as float16 (a plain copy, bits unchanged)
+        if dist.get_backend(group) == "gloo" and dt in (torch.int16, torch.uint8, torch.int8):
+            src = src.to(torch.int32)
+        elif dt == torch.int16:
+            src = src.view(torch.float16)
+        out = torch.empty((total,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        dist.all_to_all_single(out, src, output_split_sizes=recv_l, input_split_sizes=send_l, group=group)
+        out = out.to(dt) if out.dtype == torch.int32 and dt != torch.int32 else out.view(dt)
+        return out.to(dev) if host else out
+
+    cols = {c: swap(t) for c, t in binned.items()}
+    tie = swap(tiebreak) if tiebreak is not None else None
+    return cols, tie, [int(x) for x in recv_l]
+
+
 def gather_rows(tensors: Sequence[torch.Tensor], dst: int = 0, group=None) -> Optional[List[torch.Tensor]]:
     """Concatenate each [rows_r, k] tensor over ranks in rank order; result on ``dst`` only."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:

@@ -220,6 +220,54 @@ class Engine:
                                          self._stream()))
         return int(out.value)
 
+    # ---- cell bins exchanged between devices (SplitBam's bins, bam.py:439-480; exchange.h) ----
+    def bin_records(self, cols, dims: Dims, n_bins: int, tiebreak: Optional[torch.Tensor] = None,
+                    bin_of_cell: Optional[torch.Tensor] = None):
+        """Records grouped by the bin of their cell, input order kept inside a bin (sct_bin_records):
+        (binned columns, the tiebreak carried along or None, device int64 [n_bins] records per bin).
+        Bins are contiguous cell-id ranges unless ``bin_of_cell`` (device uint8 per cell id) is given."""
+        if not 1 <= int(n_bins) <= N.SCT_MAX_BINS:
+            raise ValueError("n_bins must be in [1, %d]" % N.SCT_MAX_BINS)
+        rec = records_struct(cols)
+        out = {c: torch.empty_like(cols[c]) for c in N.RECORD_COLUMNS}
+        orec = records_struct(out)
+        tie_out = torch.empty_like(tiebreak) if tiebreak is not None else None
+        plan = self._plan(rec.n, "cell", "exact", dims)
+        nbytes = ctypes.c_size_t(0)
+        N.check(self.lib.sct_bin_workspace_size(ctypes.byref(plan), int(n_bins), ctypes.byref(nbytes)))
+        ws = torch.empty(max(1, int(nbytes.value)), dtype=torch.uint8, device=self.device)
+        counts = torch.empty(int(n_bins), dtype=torch.int64, device=self.device)
+        ptr = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
+        N.check(self.lib.sct_bin_records(ctypes.byref(plan), ctypes.byref(rec), ptr(tiebreak), ptr(bin_of_cell),
+                                         int(n_bins), ctypes.byref(orec), ptr(tie_out), ptr(counts),
+                                         ctypes.c_void_p(ws.data_ptr()), ws.numel(), self._stream()))
+        return out, tie_out, counts
+
+    def exchange_counts(self, counts: torch.Tensor, comm) -> torch.Tensor:
+        """Every rank's bin counts swapped over the communicator (sct_exchange_counts): device int64
+        [n_ranks], entry p = the records rank p sends here."""
+        recv = torch.empty_like(counts)
+        N.check(self.lib.sct_exchange_counts(ctypes.c_void_p(counts.data_ptr()), ctypes.c_void_p(recv.data_ptr()),
+                                             int(counts.numel()), ctypes.c_void_p(comm), self._stream()))
+        return recv
+
+    def exchange_records(self, binned, tiebreak, send_counts, recv_counts, comm):
+        """Bin p of this rank to rank p, rank p's bin for this rank received in rank order
+        (sct_exchange_records over RCCL); send / recv counts are host sequences.  Returns (columns,
+        tiebreak or None)."""
+        n_ranks = len(send_counts)
+        total = int(sum(int(c) for c in recv_counts))
+        out = {c: torch.empty(total, dtype=_TORCH_DTYPES[c], device=self.device) for c in N.RECORD_COLUMNS}
+        tie_out = torch.empty(total, dtype=torch.int32, device=self.device) if tiebreak is not None else None
+        rec, orec = records_struct(binned), records_struct(out)
+        sc = (ctypes.c_int64 * n_ranks)(*[int(c) for c in send_counts])
+        rc = (ctypes.c_int64 * n_ranks)(*[int(c) for c in recv_counts])
+        N.check(self.lib.sct_exchange_records(
+            ctypes.byref(rec), ctypes.c_void_p(tiebreak.data_ptr()) if tiebreak is not None else None, sc, rc, n_ranks,
+            ctypes.byref(orec), ctypes.c_void_p(tie_out.data_ptr()) if tie_out is not None else None,
+            ctypes.c_void_p(comm), self._stream()))
+        return out, tie_out
+
     # ---- count matrix (CountMatrix.from_sorted_tagged_bam, count.py:134-328) ----
     def count_matrix(self, cell: torch.Tensor, umi: torch.Tensor, gene: torch.Tensor, xf: torch.Tensor,
                      qhead: torch.Tensor, gene_col: torch.Tensor, n_cell_ids: int, n_umi_ids: int, cell_none: int,

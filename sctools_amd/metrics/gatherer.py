@@ -143,6 +143,27 @@ class GatherGeneMetrics(MetricGatherer):
             write_rows(out, "gene", cols, ints, floats)
 
 
+def write_rows_of_ids(writer: MetricCSVWriter, mode: str, cols: columnar.Columns, ints: np.ndarray,
+                      floats: np.ndarray, ids: np.ndarray) -> None:
+    """Rows whose entity ids are given (records re-sorted on the device: no file position to look up)."""
+    names_of = cols.cells.names if mode == "cell" else cols.genes.names
+    names = [names_of[i] for i in ids.tolist()]
+    keep, kept = R.select_rows(mode, ints, names)
+    writer.write_bytes(R.format_rows_bytes(mode, kept, ints[keep], floats[keep]))
+
+
+def query_name_ranks(bam_file: str, mode: str):
+    """(rank of each record's query name among the file's sorted names, number of names): the last
+    field of TagSortBam's order (bam.py:638-709), decoded on the host (bamdec.cpp sort-key mode).
+    SAM input: (None, 0) -- ties then keep input order."""
+    if mode != "rb":
+        return None, 0
+    from sctools_amd import bamnative
+
+    arrays, names = bamnative.decode(bam_file, "sortkeys")
+    return arrays["qname"], max(1, len(names[3]))
+
+
 def write_grouped_gene_rows(writer: MetricCSVWriter, cols: columnar.Columns, ints: np.ndarray,
                             floats: np.ndarray) -> None:
     """Gene rows indexed by gene id: ids with reads, multi-gene values skipped, in id order (the
@@ -172,11 +193,21 @@ class GatherCellAndGeneMetrics(MetricGatherer):
         from sctools_amd import multigpu
 
         cols = self._columns(mode, columnar.MODE_CELL)
-        (ci, cf), (gi, gf) = multigpu.compute_cell_and_gene_rows(cols, self._mitochondrial_gene_ids,
-                                                                 self._float_mode, self._devices)
-        with MetricCSVWriter(self._output_stem, self._compress) as out:
-            out.write_header(vars(CellMetrics()))
-            write_rows(out, "cell", cols, ci, cf)
+        if multigpu.cells_twice(cols):
+            # not cell-sorted: the rows of TagSortBam by (CB, UB, GE, query name) + GatherCellMetrics
+            # (and by (GE, CB, UB) + GatherGeneMetrics), the cell bins swapped between the devices
+            tie, n_tie = (None, 0) if self._float_mode == "exact" else query_name_ranks(self.bam_file, mode)
+            (ci, cf, ids), (gi, gf) = multigpu.sorted_cell_and_gene_rows(
+                cols, self._mitochondrial_gene_ids, self._float_mode, self._devices, tie, n_tie)
+            with MetricCSVWriter(self._output_stem, self._compress) as out:
+                out.write_header(vars(CellMetrics()))
+                write_rows_of_ids(out, "cell", cols, ci, cf, ids)
+        else:
+            (ci, cf), (gi, gf) = multigpu.compute_cell_and_gene_rows(cols, self._mitochondrial_gene_ids,
+                                                                     self._float_mode, self._devices)
+            with MetricCSVWriter(self._output_stem, self._compress) as out:
+                out.write_header(vars(CellMetrics()))
+                write_rows(out, "cell", cols, ci, cf)
         with MetricCSVWriter(self._gene_output_stem, self._compress) as out:
             out.write_header(vars(GeneMetrics()))
             write_grouped_gene_rows(out, cols, gi, gf)

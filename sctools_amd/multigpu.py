@@ -173,6 +173,8 @@ class DeviceGroup:
         """fn(rank) on every rank, each in its own thread with its device current.  If a rank raises,
         the group's collective is skipped (or aborted) on every rank and the error is re-raised here."""
         self._run = GroupRun(self.size, abort_fn=self.abort)
+        self._slots = [None] * self.size
+        self._xslots = [None] * self.size
         try:
             return self._run.run(fn, setup=lambda r: torch.cuda.device(self.devices[r]))
         finally:
@@ -241,6 +243,56 @@ class DeviceGroup:
         if rank == 0:
             self._slots = [None] * self.size
 
+    def exchange(self, rank: int, binned: dict, tiebreak: Optional[torch.Tensor], counts: torch.Tensor):
+        """The cell-bin swap (call from every rank's thread, inside run()): bin p of every rank's
+        ``binned`` records (``counts``: device int64 [size], Engine.bin_records) goes to rank p; each rank
+        receives its bin of rank 0, then of rank 1, ... -- file order when rank r holds the r-th part of
+        the file.  RCCL send / recv (sct_exchange_records); shards sharing a device copy in device
+        memory.  Returns (columns, tiebreak or None) on the rank's device."""
+        g = self._run
+        if g is None:
+            raise RuntimeError("exchange is called from the ranks of DeviceGroup.run")
+        if counts.numel() != self.size:
+            raise ValueError("%d bin counts for %d ranks" % (counts.numel(), self.size))
+        g.before_collective(rank)
+        eng = self.engines[rank]
+        stream = torch.cuda.current_stream(eng.device)
+        if self.shared:
+            return self._local_exchange(rank, binned, tiebreak, counts)
+        comm = self._rank_comm(rank)
+        recv = eng.exchange_counts(counts, comm)
+        done = torch.cuda.Event()
+        done.record(stream)
+        g.wait(rank, done.query)  # (a peer that failed never sends: no blocking read before this)
+        send_h, recv_h = counts.cpu().tolist(), recv.cpu().tolist()
+        out = eng.exchange_records(binned, tiebreak, send_h, recv_h, comm)
+        done = torch.cuda.Event()
+        done.record(stream)
+        g.wait(rank, done.query)
+        return out
+
+    def _local_exchange(self, rank: int, binned: dict, tiebreak, counts):
+        """Shards on shared devices: the same swap by device copies."""
+        g = self._run
+        dev = self.engines[rank].device
+        torch.cuda.current_stream(dev).synchronize()
+        self._xslots[rank] = (binned, tiebreak, counts.cpu().tolist())
+        g.before_collective(rank)  # every rank's bins are ready
+        cols, ties = {c: [] for c in binned}, []
+        for p in range(self.size):
+            b, t, cnt = self._xslots[p]
+            lo = int(sum(cnt[:rank]))
+            hi = lo + int(cnt[rank])
+            for c in cols:
+                cols[c].append(b[c][lo:hi].to(dev))
+            if t is not None:
+                ties.append(t[lo:hi].to(dev))
+        out = {c: torch.cat(v) for c, v in cols.items()}
+        tie = torch.cat(ties) if tiebreak is not None else None
+        torch.cuda.current_stream(dev).synchronize()
+        g.before_collective(rank)  # every rank has its pieces
+        return out, tie
+
     def abort(self) -> None:
         """A rank failed: cancel the collective on every communicator (ncclCommAbort).  The group
         stays aborted: a rank that reaches comms() afterwards raises GroupAborted instead of
@@ -308,6 +360,11 @@ def _cells_twice(cols) -> bool:
         return int(torch.bincount(heads.long()).max().item()) > 1
     heads = cell[np.concatenate(([0], np.flatnonzero(cell[1:] != cell[:-1]) + 1))]
     return np.bincount(heads).max() > 1
+
+
+def cells_twice(cols) -> bool:
+    """True when a cell barcode forms two runs: the records are not cell-sorted."""
+    return _cells_twice(cols)
 
 
 def _shard_to(cols: columnar.Columns, lo: int, hi: int, device) -> dict:
@@ -402,3 +459,78 @@ def compute_cell_and_gene_rows(cols: columnar.Columns, mitochondrial_gene_ids=fr
         parts = g.run(rank_rows)
     cell = (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
     return cell, parts[0][2]
+
+
+def sorted_cell_and_gene_rows(cols, mitochondrial_gene_ids=frozenset(), float_mode: str = "exact", devices=1,
+                              tiebreak: Optional[np.ndarray] = None, n_tiebreak_ids: int = 0):
+    """Cell rows and grouped gene rows of records in ANY order: the cell rows TagSortBam by
+    (CB, UB, GE[, query name]) followed by GatherCellMetrics writes, the gene rows those of
+    TagSortBam by (GE, CB, UB) + GatherGeneMetrics -- the reference's SplitBam + TagSortBam +
+    Calculate*Metrics + Merge*Metrics route for an unsorted BAM (bam.py:361-488, platform.py:55-97,
+    merge.py:59-191) on the devices:
+
+    * rank r takes the r-th part of the records (its decoded shard, or a contiguous range) and bins
+      them by cell: contiguous ranges of barcode ranks, one per rank (sct_bin_records);
+    * the ranks swap bins over RCCL (sct_exchange_records): rank r then holds every record of its
+      cells, in file order;
+    * each rank sorts them (sct_tag_sort, the query-name rank ``tiebreak`` as the last field if
+      given, ties in input order as sorted() keeps them) and computes its cells' rows and gene
+      partials; ONE all-reduce sums the partials; rank 0 finalizes the gene rows.
+
+    Rank r's cells are the r-th barcode range, so rank order is barcode order: the concatenated
+    cell rows are in TagSortBam's order.  Returns ((ints, floats, cell ids), (gene ints, gene floats))."""
+    from sctools_amd import engine as E
+
+    mito, _ = cols.gene_flags(mitochondrial_gene_ids)
+    dims = _dims(cols)
+    if tiebreak is not None:
+        tiebreak = np.ascontiguousarray(tiebreak, dtype=np.int32)
+        n_all = cols.offsets[-1] if isinstance(cols, columnar.ShardedColumns) else int(cols.arrays["cell"].shape[0])
+        if tiebreak.shape[0] != n_all:
+            raise ValueError("tiebreak has %d entries for %d records" % (tiebreak.shape[0], n_all))
+        if n_tiebreak_ids <= 0:
+            raise ValueError("n_tiebreak_ids must be positive with a tiebreak")
+    with DeviceGroup(devices) as g:
+        bounds = _bounds(cols, "cell", g.size)
+        if g.size > N.SCT_MAX_BINS:
+            raise ValueError("at most %d devices" % N.SCT_MAX_BINS)
+        g.comms()
+
+        def rank_rows(r):
+            lo, hi = bounds[r]
+            eng = g.engines[r]
+            part = _rank_cols(cols, r, lo, hi, eng.device)
+            tie = torch.from_numpy(tiebreak[lo:hi]).to(eng.device) if tiebreak is not None else None
+            binned, btie, counts = eng.bin_records(part, dims, g.size, tie)
+            del part, tie
+            mine, mtie = g.exchange(r, binned, btie, counts)
+            del binned, btie
+            n = int(mine["cell"].shape[0])
+            srt = eng.tag_sort(mine, dims, "cell_umi_gene", mtie, n_tiebreak_ids if mtie is not None else 0) \
+                if n else mine
+            del mine, mtie
+            gm = torch.from_numpy(mito).to(eng.device)
+            if n == 0:
+                part = torch.zeros((max(1, dims.n_gene_ids), N.SCT_NP), dtype=torch.int64, device=eng.device)
+                ci = np.zeros((0, N.SCT_NI), np.int64)
+                cf = np.zeros((0, N.SCT_NF), np.float64)
+                ids = np.zeros(0, np.int64)
+            else:
+                if float_mode == "exact":
+                    ci, cf, part = eng.cell_and_gene(srt, dims, gm)
+                else:
+                    gx = torch.zeros_like(gm)
+                    ci, cf = eng.compute(srt, "cell", dims, gm, gx, float_mode=float_mode)
+                    part = eng.gene_partials(srt, dims)
+                ids = srt["cell"][ci[:, N.I_ENTITY]].to(torch.int64).cpu().numpy()
+                ci, cf = ci.cpu().numpy(), cf.cpu().numpy()
+            g.allreduce_partials(r, part)
+            gene = None
+            if r == 0:
+                gi, gf = eng.finalize_partials(part)
+                gene = (gi.cpu().numpy(), gf.cpu().numpy())
+            return ci, cf, ids, gene
+
+        parts = g.run(rank_rows)
+    cell = tuple(np.concatenate([p[k] for p in parts]) for k in range(3))
+    return cell, parts[0][3]

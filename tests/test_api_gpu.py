@@ -160,12 +160,14 @@ def test_cell_and_gene_rows_from_one_cell_sorted_pass(tmp_path, float_mode):
     H.assert_csv_close(_read(gstem + ".csv.gz"), H.golden_text("small-gene-sorted", "gene"), rel=1e-9)
 
 
-def test_cell_and_gene_rows_need_cell_sorted_input(tmp_path):
-    from sctools_amd.metrics import GatherCellAndGeneMetrics
+def test_cell_sorted_pass_refuses_unsorted_input():
+    """The one-pass route (no sort) needs every cell in one run; GatherCellAndGeneMetrics sends an
+    unsorted file through the bin exchange + tag sort instead (tests/test_gpu_exchange.py)."""
+    from sctools_amd import columnar, multigpu
 
+    cols = columnar.columnarize(os.path.join(BAM_DIR, "unsorted.bam"), "rb", "cell")
     with pytest.raises(ValueError, match="cell-sorted"):
-        GatherCellAndGeneMetrics(os.path.join(BAM_DIR, "unsorted.bam"), str(tmp_path / "c"),
-                                 str(tmp_path / "g")).extract_metrics()
+        multigpu.compute_cell_and_gene_rows(cols, float_mode="exact", devices=[0])
 
 
 def test_allreduce_c_abi_with_own_communicator():
