@@ -161,13 +161,42 @@ __device__ __forceinline__ void welford_store(double* F, int st, double mean, do
 // 32 contiguous bytes (a wave's load touches 16 lines, not 64).  The chains below load one double
 // per record; xs holds kWfPad records of slack past n for their unclamped reads.
 constexpr int kWfPad = 64;
+constexpr int kWfHeadGroups = 4;
+constexpr int kWfHeadEnts = kWfHeadGroups * (kWave / 4);
+static_assert(kWfHeadEnts == kWave, "one lane per head entity");
+// (round 5) records of the head entities are skipped: k_welford_x_ents wrote their samples on the
+// head stream, whose chains read them while this kernel runs (the same bits rewritten
+// under a concurrent read).  The first wave finds the head ranges that meet the block's records.
 template <bool kCell>
-__global__ void __launch_bounds__(kBlock) k_welford_x(RecCols r, int64_t n, double* __restrict__ xs) {
+__global__ void __launch_bounds__(kBlock) k_welford_x(RecCols r, int64_t n, double* __restrict__ xs,
+                                                      const int64_t* __restrict__ ent_start, int64_t n_ent,
+                                                      const uint32_t* __restrict__ order,
+                                                      const uint32_t* __restrict__ n_head) {
   __shared__ double s_rcp[kRcpN];
+  __shared__ int64_t s_lo[kWfHeadEnts], s_hi[kWfHeadEnts];
+  __shared__ uint64_t s_meet;
   fill_rcp(s_rcp);
+  const int64_t b0 = (int64_t)blockIdx.x * kBlock, b1 = b0 + kBlock < n ? b0 + kBlock : n;
+  if (threadIdx.x < kWave) {
+    const int k = threadIdx.x, m = (int)*n_head;
+    int64_t lo = 0, hi = 0;
+    if (k < m) {
+      const int64_t e = order[k];
+      lo = ent_start[e];
+      hi = (e + 1 < n_ent) ? ent_start[e + 1] : n;
+    }
+    s_lo[k] = lo;
+    s_hi[k] = hi;
+    const uint64_t meet = __ballot(k < m && lo < b1 && hi > b0);
+    if (k == 0) s_meet = meet;
+  }
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t i = b0 + threadIdx.x;
   if (i >= n) return;
+  for (uint64_t mk = s_meet; mk; mk &= mk - 1) {
+    const int k = __ffsll((unsigned long long)mk) - 1;
+    if (i >= s_lo[k] && i < s_hi[k]) return;  // a head entity's record
+  }
   double x[4];
   welford_samples<kCell>(r, i, s_rcp, x);
   double2* o = reinterpret_cast<double2*>(xs + 4 * i);
@@ -180,8 +209,6 @@ __global__ void __launch_bounds__(kBlock) k_welford_x(RecCols r, int64_t n, doub
 // on another stream.  k_welford_split gives the head groups their own queue (ctl_head) and starts
 // the main queue after them; k_welford_x_ents computes the samples of the head entities' records
 // only (a grid-stride loop over their concatenation).
-constexpr int kWfHeadGroups = 4;
-constexpr int kWfHeadEnts = kWfHeadGroups * (kWave / 4);
 __global__ void k_welford_split(WelfordCtl* __restrict__ ctl, WelfordCtl* __restrict__ ctl_head) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const uint32_t nb = ctl->n_big;

@@ -1229,6 +1229,16 @@ int open_impl(const char* path, int32_t part, int32_t n_parts, int64_t first_sta
   };
   G->pm_lo = cut(part);
   G->pm_hi = std::max(G->pm_lo, cut(part + 1));
+  if (G->pm_lo == G->pm_hi) {
+    // an empty part (more parts than members, or a header longer than the part's share): no
+    // records, and transparent to the landing chain -- it starts and lands where it is told to
+    // (the previous part's landing may lie past its member boundary), else at that boundary
+    G->first_abs = G->land_abs = first_start >= 0 ? first_start : (int64_t)G->O[G->pm_lo];
+    G->t[0] = now() - t0;
+    *n_records = 0;
+    *out = G.release();
+    return SCT_BAM_OK;
+  }
   uint32_t wmH = 0;
   uint64_t wH = kUnknown;
   if (part == 0) {
@@ -1238,13 +1248,6 @@ int open_impl(const char* path, int32_t part, int32_t n_parts, int64_t first_sta
     if ((uint64_t)first_start < G->O[G->pm_lo] || (uint64_t)first_start > G->O[G->pm_hi])
       return gfail(SCT_BAM_EIO, "first_start outside the part");
     wH = (uint64_t)first_start - G->O[G->pm_lo];
-  }
-  if (G->pm_lo == G->pm_hi) {  // an empty part (more parts than members): no records
-    G->first_abs = G->land_abs = (int64_t)G->O[G->pm_lo];
-    G->t[0] = now() - t0;
-    *n_records = 0;
-    *out = G.release();
-    return SCT_BAM_OK;
   }
   plan_windows(G.get(), wmH, wH, window_bytes());
   G->t[0] = now() - t0;

@@ -434,7 +434,8 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
              (const uint32_t*)worder, (const WelfordCtl*)wch, xs);
       LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfHeadGroups), dim3(kBlock), s2, ent_start, n_ent, n,
                (const uint32_t*)worder, wch, (const double*)xs, out_f);
-      LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s3, rc2, n, xs);
+      LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s3, rc2, n, xs, ent_start, n_ent,
+               (const uint32_t*)worder, (const uint32_t*)&wch->n_big);
       LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,
                (const uint32_t*)worder, wc, (const double*)xs, out_f);
     } else {
@@ -442,7 +443,8 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
              (const uint32_t*)worder, (const WelfordCtl*)wch, xs);
       LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfHeadGroups), dim3(kBlock), s2, ent_start, n_ent, n,
                (const uint32_t*)worder, wch, (const double*)xs, out_f);
-      LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s3, rc2, n, xs);
+      LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s3, rc2, n, xs, ent_start, n_ent,
+               (const uint32_t*)worder, (const uint32_t*)&wch->n_big);
       LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,
                (const uint32_t*)worder, wc, (const double*)xs, out_f);
     }

@@ -109,6 +109,13 @@ class _Handle:
         _check(self.L.sct_gbam_part_bounds(self.h, ctypes.byref(a), ctypes.byref(b)))
         return int(a.value), int(b.value)
 
+    def dictionary_size(self, which: int) -> int:
+        """Entries of dictionary ``which`` (the count alone: no copy of its strings)."""
+        cnt, by, off, hn = ctypes.c_int64(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int32()
+        self.L.sct_gbam_dictionary(self.h, which, ctypes.byref(cnt), ctypes.byref(by), ctypes.byref(off),
+                                   ctypes.byref(hn))
+        return int(cnt.value)
+
     def dictionary(self, which: int, lazy: bool = True):
         cnt, by, off, hn = ctypes.c_int64(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int32()
         self.L.sct_gbam_dictionary(self.h, which, ctypes.byref(cnt), ctypes.byref(by), ctypes.byref(off),
@@ -306,7 +313,7 @@ def decode_parts(path: str, metric_mode: str, devices, timings: Optional[dict] =
         L = load()
         remaps = []
         for which in range(3):
-            sizes = [len(hs[p].dictionary(which)) for p in range(P)]
+            sizes = [hs[p].dictionary_size(which) for p in range(P)]
             arrs = [np.zeros(max(1, k), dtype=np.int32) for k in sizes]
             ptrs = (ctypes.POINTER(ctypes.c_int32) * P)(
                 *[a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)) for a in arrs])

@@ -20,15 +20,18 @@ attribute from the engine's row.  ``finalize`` of an aggregator that parsed
 nothing gives the reference's values (zero counts, 0.0 means, NaN variances
 and ratios) without a launch.
 
-Known gap: a record that raises part-way (``KeyError`` on XF or NH
-of a mapped read, ``ZeroDivisionError`` / ``TypeError`` on its qualities) is
-not buffered.  The reference has by then already fed that record to its
-molecule histogram and its UY / genomic Welford streams (and, for XF / NH, its
-fragment histogram), so a caller that *catches* the error and still calls
-``finalize()`` gets n_molecules, n_fragments and the stream means of the
-records before it only.  The gatherers never do that (the error aborts
-``extract_metrics``, as in the reference), and the integer counters the
-reference updates before the raise point are kept exactly.
+A record that raises part-way (round 5): the reference has by then fed it to some
+of its state.  A mapped read without an XF or NH tag (``KeyError``, aggregator.py:305 / 317) has
+reached its molecule and fragment histograms and its UY / genomic Welford streams (264-303), so it
+is buffered with the fields read so far before the error propagates; ``finalize()`` then takes the
+distinct counts and the streams from the engine (that record included) and keeps the host's
+integer counters, which stopped exactly where the reference's stopped.  A caller that catches the
+error and calls ``finalize()`` -- at once, or after parsing more records -- gets the reference's
+values (tests/golden/protocol: ``final_after_error``, ``final_continued``).  Remaining gap: a
+record that raises earlier -- ``KeyError`` on CR (after its CY sample, 507-520) or UY, or
+``TypeError`` / ``ZeroDivisionError`` on its qualities (after its UY sample) -- has fed only part of
+a record's streams, which the engine's record format cannot express; it is not buffered, so
+``finalize()`` after catching such an error leaves it out of the streams and distinct counts.
 """
 
 from typing import Sequence
@@ -86,11 +89,8 @@ class MetricAggregator:
         """aggregator.py:251-334, record by record: the subclass fields first, then the counters,
         raising where the reference raises.
 
-        Known gap: a record that raises part-way (a mapped read without an XF or NH tag, a record
-        past the 32-byte columnar limits) is not buffered.  The reference has by then already
-        counted it in n_reads, the molecule and fragment histograms and the quality streams, so a
-        caller that catches the error and still calls finalize() gets those metrics without that
-        record (finalize() recomputes every column from the buffered records)."""
+        A mapped read without an XF or NH tag is buffered before its KeyError propagates (the
+        reference has counted it in its histograms and streams by then; see the module docstring)."""
         for record in records:
             self._extra = (0, 0)
             self.parse_extra_fields(tags=tags, record=record)
@@ -121,17 +121,28 @@ class MetricAggregator:
                 b |= C.B_REVERSE
             if flag & 0x400:
                 b |= C.B_DUPLICATE
+            s = sum(aq)
+            gq = (s, len(aq), sum(1 for q in aq if q > 30))
             if flag & 0x4:
                 b |= C.B_UNMAPPED
             else:
-                alignment_location = record.get_tag(consts.ALIGNMENT_LOCATION_TAG_KEY)
+                try:
+                    alignment_location = record.get_tag(consts.ALIGNMENT_LOCATION_TAG_KEY)
+                except KeyError:
+                    self._buffer_partial(tags, record, gq, b, x, cg, cl, ug, ul)
+                    raise
                 if alignment_location == consts.CODING_ALIGNMENT_LOCATION_TAG_VALUE:
                     self.reads_mapped_exonic += 1
                 elif alignment_location == consts.INTRONIC_ALIGNMENT_LOCATION_TAG_VALUE:
                     self.reads_mapped_intronic += 1
                 elif alignment_location == consts.UTR_ALIGNMENT_LOCATION_TAG_VALUE:
                     self.reads_mapped_utr += 1
-                if record.get_tag(consts.NUMBER_OF_HITS_TAG_KEY) == 1:
+                try:
+                    nh = record.get_tag(consts.NUMBER_OF_HITS_TAG_KEY)
+                except KeyError:
+                    self._buffer_partial(tags, record, gq, b, x, cg, cl, ug, ul)
+                    raise
+                if nh == 1:
                     self.reads_mapped_uniquely += 1
                     b |= C.B_NH1
                 else:
@@ -144,11 +155,19 @@ class MetricAggregator:
                     self.spliced_reads += 1
                     b |= C.B_SPLICED
                 self._plus_strand_reads += not (flag & 0x10)
-            s = sum(aq)
-            if len(aq) > 0xFFFF or s > 0xFFFF or cl > 0xFF or ul > 0xFF:
+            if not _fits(gq, cl, ul):
                 raise ValueError("record %s exceeds the 32-byte columnar limits" % getattr(record, "query_name", "?"))
-            num = (record.reference_id, record.pos, s, len(aq), sum(1 for q in aq if q > 30), b, x, cg, cl, ug, ul)
+            num = (record.reference_id, record.pos) + gq + (b, x, cg, cl, ug, ul)
             self._buffered.append((tuple(tags), num))
+
+    def _buffer_partial(self, tags, record, gq, b, x, cg, cl, ug, ul) -> None:
+        """A mapped read about to raise KeyError on XF or NH (aggregator.py:305 / 317): buffered as
+        the reference has consumed it -- its molecule and fragment keys and its stream samples -- so
+        the engine's distinct counts and streams include it; the XF / NH counters it never reached are
+        the host's (_fill keeps them).  A record past the columnar limits stays out (the KeyError
+        still propagates)."""
+        if _fits(gq, cl, ul):
+            self._buffered.append((tuple(tags), (record.reference_id, record.pos) + gq + (b, x, cg, cl, ug, ul)))
 
     def parse_extra_fields(self, tags: Sequence[str], record) -> None:
         """Per-record hook of the subclasses (aggregator.py:336-340)."""
@@ -176,12 +195,29 @@ class MetricAggregator:
                 setattr(self, name, _NAN)
 
     def _fill(self, ints: np.ndarray, floats: np.ndarray) -> None:
+        """Every public attribute from the engine's row, except the per-record counters the host keeps
+        in the reference's order (they differ from the engine's only after a caught error)."""
         for name, kind, slot in R.columns_for(self._MODE):
+            if name in _HOST_COUNTERS:
+                continue
             v = ints[slot] if kind == R.I else floats[slot]
             setattr(self, name, int(v) if kind == R.I else float(v))
 
     def finalize(self) -> None:
         self._run_engine()
+
+
+# counters parse_molecule / parse_extra_fields keep record by record (aggregator.py:259-334, 507-527)
+_HOST_COUNTERS = frozenset((
+    "n_reads", "noise_reads", "perfect_molecule_barcodes", "reads_mapped_exonic", "reads_mapped_intronic",
+    "reads_mapped_utr", "reads_mapped_uniquely", "reads_mapped_multiple", "duplicate_reads", "spliced_reads",
+    "antisense_reads", "perfect_cell_barcodes", "reads_mapped_intergenic", "reads_unmapped",
+    "reads_mapped_too_many_loci"))
+
+
+def _fits(gq, cl, ul) -> bool:
+    """The 32-byte record's field widths (uint16 genomic quality sums, uint8 barcode lengths)."""
+    return gq[1] <= 0xFFFF and gq[0] <= 0xFFFF and cl <= 0xFF and ul <= 0xFF
 
 
 def _perfect_umi(record) -> bool:

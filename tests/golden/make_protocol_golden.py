@@ -12,9 +12,13 @@ Each case names an entity of a bundled BAM (its records in file order) and, opti
 record to damage (a tag dropped, or no base qualities).  Recorded: the integer attributes after
 each record, the exception type a record raised (the case stops there), and, for cases without
 an error, every public attribute after ``finalize()`` as ``str`` (the CSV text, writer.py:96).  An empty aggregator's
-``finalize()`` is recorded too.
+``finalize()`` is recorded too.  For a case whose damaged record raised, two more states (round 5):
+``final_after_error`` -- the caller catches the exception and calls ``finalize()`` at once -- and
+``final_continued`` -- the caller catches it, parses the entity's remaining records, then
+``finalize()`` -- each every public attribute as ``str`` (or the exception ``finalize`` raised).
 """
 
+import copy
 import json
 import os
 import sys
@@ -94,6 +98,14 @@ def damaged(rec, damage):
     return seg
 
 
+def finalized(agg):
+    try:
+        agg.finalize()
+    except Exception as e:  # noqa: BLE001 -- recorded
+        return {"raised": type(e).__name__}
+    return {k: str(v) for k, v in vars(agg).items() if not k.startswith("_")}
+
+
 def attrs(kind):
     return INT_ATTRS + (CELL_INT_ATTRS if kind == "cell" else [])
 
@@ -118,12 +130,18 @@ def main():
             steps.append(state(agg, kind))
             if raised:
                 break
-        final = None
+        final = final_after = final_cont = None
         if raised is None:
             agg.finalize()
             final = {k: str(v) for k, v in vars(agg).items() if not k.startswith("_")}
+        else:
+            final_after = finalized(copy.deepcopy(agg))
+            for t, r in items[len(steps):]:
+                agg.parse_molecule(tags=t, records=[damaged(r, None)])
+            final_cont = finalized(agg)
         out.append({"kind": kind, "bam": bam, "entity": ent, "entity_name": name, "bad_record": bad,
-                    "damage": damage, "attrs": attrs(kind), "steps": steps, "raised": raised, "final": final})
+                    "damage": damage, "attrs": attrs(kind), "steps": steps, "raised": raised, "final": final,
+                    "final_after_error": final_after, "final_continued": final_cont})
     empty = {}
     for kind in ("cell", "gene"):
         agg = CellMetrics() if kind == "cell" else GeneMetrics()

@@ -222,6 +222,50 @@ def test_aggregator_protocol_golden_finalize():
     assert done >= 8
 
 
+# damaged records whose partial state the aggregator reproduces: CY missing (nothing consumed yet)
+# and a mapped read without XF / NH (buffered as far as the reference consumed it)
+EXACT_AFTER_ERROR = ("drop:CY", "drop:XF", "drop:NH")
+
+
+def _same_final(got, want, label):
+    import math
+
+    assert list(got) == list(want), label
+    for k, v in got.items():
+        w = want[k]
+        if w == "nan":
+            assert isinstance(v, float) and math.isnan(v), (label, k)
+        else:
+            assert str(v) == w, (label, k, v, w)
+
+
+def test_finalize_after_a_caught_error_matches_reference():
+    """a caller catches the damaged record's exception and calls finalize() at once
+    (final_after_error) or after parsing the entity's remaining records (final_continued); every
+    public attribute equals the reference's (tests/golden/protocol, make_protocol_golden.py)."""
+    import copy
+
+    import test_protocol_cpu as P
+
+    done = 0
+    for case in P.CASES:
+        if case["raised"] is None or case["damage"] not in EXACT_AFTER_ERROR:
+            continue
+        agg, steps, raised = P.replay(case)
+        assert raised == case["raised"]
+        label = (case["kind"], case["bam"], case["entity"], case["damage"])
+        after = copy.deepcopy(agg)
+        after.finalize()
+        _same_final({k: v for k, v in vars(after).items() if not k.startswith("_")}, case["final_after_error"], label)
+        _, items = P.entity_records(case["kind"], case["bam"], case["entity"])
+        for t, r in items[len(steps):]:
+            agg.parse_molecule(tags=t, records=[r])
+        agg.finalize()
+        _same_final({k: v for k, v in vars(agg).items() if not k.startswith("_")}, case["final_continued"], label)
+        done += 1
+    assert done >= 6
+
+
 @pytest.mark.parametrize("bam", H.BAMS)
 @pytest.mark.parametrize("kind", ["cell", "gene"])
 def test_gatherers_three_shards_on_one_device(tmp_path, bam, kind):

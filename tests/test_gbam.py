@@ -299,3 +299,25 @@ def test_parts_decode_matches_host(tmp_path, monkeypatch, n_parts, window):
     assert np.array_equal(sc.host().arrays["cell"], want["cell"])
     idx = np.array([0, 5, sc.n // 2, sc.n - 1])
     assert np.array_equal(sc.column_at("gene", idx), want["gene"][idx])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_parts,block", [(7, 65280), (12, 30000), (5, 65280)])
+def test_parts_with_empty_parts_match_host(tmp_path, n_parts, block):
+    """More parts than record members: some parts own no member and decode no record.
+    An empty part starts and lands where the previous part's walk landed (records cross member
+    boundaries, so that landing can lie past the empty part's member boundary) -- the next part is
+    checked against it -- and the parts still concatenate to the host decoder's columns."""
+    raw = payload(os.path.join(GOLD, "small-cell-sorted.bam"))
+    path = str(tmp_path / "e.bam")
+    rebgzf(raw, path, level=6, block=block)
+    t = {}
+    got = gbam.decode_parts(path, "cell", ["cuda:0"] * n_parts, timings=t)
+    assert got is not None, gbam.last_error()
+    assert len(t["parts"]) == n_parts and min(t["parts"]) == 0, t["parts"]
+    shards, names = got
+    want, want_names = host(path, "cell")
+    assert [d.names for d in names] == want_names
+    for c, a in want.items():
+        g = np.concatenate([sh[c].cpu().numpy().view(a.dtype) for sh in shards])
+        assert np.array_equal(g, a), c

@@ -105,3 +105,12 @@ def test_protocol_golden_covers_the_error_paths():
     raised = {c["raised"] for c in CASES}
     assert {"KeyError", "TypeError", None} <= raised
     assert any(c["kind"] == "gene" and c["raised"] for c in CASES)
+
+
+def test_protocol_golden_records_finalize_after_caught_errors():
+    """Every raising case carries the reference's finalize() after the caught error, at once and after
+    the entity's remaining records (make_protocol_golden.py, round 5)."""
+    for c in CASES:
+        if c["raised"]:
+            assert c["final_after_error"] and c["final_continued"], c["damage"]
+            assert "n_molecules" in c["final_after_error"]
