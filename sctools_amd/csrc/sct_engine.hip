@@ -168,11 +168,13 @@ int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool du
   uint64_t* tc = at<uint64_t>(ws, L.tile_cnt);
   uint64_t* sc = at<uint64_t>(ws, L.scalars);
   uint32_t* seen = nullptr;
+  FillBatch fb;
   if (dup_check) {
     seen = at<uint32_t>(ws, L.seen);
-    HIPCHK(hipMemsetAsync(seen, 0, sizeof(uint32_t) * (size_t)n_ids, s));
+    fb.add(seen, sizeof(uint32_t) * (size_t)n_ids);
   }
-  HIPCHK(hipMemsetAsync(sc, 0, 2 * sizeof(uint64_t), s));
+  fb.add(sc, 2 * sizeof(uint64_t));
+  if (int rc = launch_fills(fb, s)) return rc;
   if (((uintptr_t)ent & 15) == 0) {
     LAUNCH_N("heads", n, k_heads4, dim3((unsigned)tiles), dim3(kBlock), s, ent, n, tc, seen, (uint32_t)n_ids, sc + 1);
   } else {
@@ -208,6 +210,13 @@ int launch_hash_tile(bool cell, bool gene, dim3 grid, hipStream_t s, const uint1
 // per-entity digit counts, level 0, then level 1's classification with a grid sized for the most
 // segments there can be (the device count bounds it): l1.hist then holds every segment child's start.
 // No host wait.
+// (its buffers -- bdesc, the level-0 counters, l1.hist -- are zeroed by the caller: level1_fills)
+void level1_fills(const Layout& L, void* ws, int64_t n, int64_t n_ent, const L1Plan& l1, FillBatch& fb) {
+  fb.add(at<uint16_t>(ws, L.bdesc), sizeof(uint16_t) * (size_t)n);
+  fb.add(level0_ctr(ws, L), 3 * sizeof(uint32_t));
+  fb.add(l1.hist, sizeof(uint32_t) * kRadix * (size_t)n_ent);
+}
+
 int bucket_level1_plan(const Layout& L, void* ws, const KeyCols& kc, int64_t n, int64_t n_ent, const Bits& b,
                        int64_t* ent_start, const L1Plan& l1, hipStream_t s) {
   uint16_t* bdesc = at<uint16_t>(ws, L.bdesc);
@@ -215,9 +224,6 @@ int bucket_level1_plan(const Layout& L, void* ws, const KeyCols& kc, int64_t n, 
   BucketCtl* ctl = bucket_ctl(ws, L);
   uint32_t* ctr0 = level0_ctr(ws, L);
   const int KB = b.k1 + b.k2 + b.h;
-  HIPCHK(hipMemsetAsync(bdesc, 0, sizeof(uint16_t) * (size_t)n, s));
-  HIPCHK(hipMemsetAsync(ctr0, 0, 3 * sizeof(uint32_t), s));
-  HIPCHK(hipMemsetAsync(l1.hist, 0, sizeof(uint32_t) * kRadix * (size_t)n_ent, s));
   LAUNCH_N("level1_plan", n, k_level1_plan, dim3((unsigned)cdiv(n, kKTile)), dim3(kBlock), s, kc.ent, kc.k1, kc.n_k1, n,
          (const uint64_t*)at<uint64_t>(ws, L.tile_cnt), b, b.k1 - kRadixBits, ent_start, l1);
   LAUNCH("bucket_level0", k_bucket_level0, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, ent_start, n_ent, n,
@@ -531,13 +537,18 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     l1 = L1Plan{at<uint32_t>(ws, L.ent_hist), at<uint32_t>(ws, L.l1_toff), at<uint2>(ws, L.l1_tslot),
                 at<Pay>(ws, L.pay_b)};
   const uint8_t* mito = gene_is_mito;
+  // every buffer the step zeroes before its first kernel, in one launch
+  FillBatch fb;
   if (cell && !mito) {
     uint8_t* z = at<uint8_t>(ws, L.zero_mito);
-    HIPCHK(hipMemsetAsync(z, 0, (size_t)plan->n_gene_ids, s));
+    fb.add(z, (size_t)plan->n_gene_ids);
     mito = z;
   }
-  HIPCHK(hipMemsetAsync(partials, 0, sizeof(int64_t) * SCT_NP * (size_t)n_ent, s));
-  if (gene) HIPCHK(hipMemsetAsync(gcounts, 0, sizeof(uint32_t) * (size_t)L.n_buckets, s));
+  fb.add(partials, sizeof(int64_t) * SCT_NP * (size_t)n_ent);
+  if (gene) {
+    fb.add(gcounts, sizeof(uint32_t) * (size_t)L.n_buckets);
+    fb.add(gene_partials, sizeof(int64_t) * SCT_NP * (size_t)plan->n_gene_ids);  // (written by gene_reduce only)
+  }
 
   // 1. input order: runs, keys, additive metrics (+ gene-bucket counts per tile)
   const dim3 tgrid((unsigned)cdiv(n, kKTile));  // key-pass blocks (tile offsets are per kTile)
@@ -545,7 +556,14 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   // exact mean / variance lanes of the output rows ride along in the same launch
   const bool streams = exact && out_i;
   BucketCtl* ctl = bucket_ctl(ws, L);
-  HIPCHK(hipMemsetAsync(ctl, 0, sizeof(BucketCtl), s));
+  fb.add(ctl, sizeof(BucketCtl));
+  // gene payload format: narrow (8 B) unless an operand does not fit (checked by the exact-stream
+  // pass; without it the wide format is used)
+  uint32_t* gwide = reinterpret_cast<uint32_t*>(at<uint64_t>(ws, L.scalars) + 16);
+  fb.add(gwide, sizeof(uint32_t), streams ? 0 : 1);
+  if (planned) level1_fills(L, ws, n, n_ent, l1, fb);
+  rc = launch_fills(fb, s);
+  if (rc) return rc;
   if (planned) {
     rc = bucket_level1_plan(L, ws, kc, n, n_ent, b, ent_start, l1, s);
     if (rc) return rc;
@@ -560,10 +578,6 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     if (rc) return rc;
   }
 
-  // gene payload format: narrow (8 B) unless an operand does not fit (checked by the exact-stream
-  // pass; without it the wide format is used)
-  uint32_t* gwide = reinterpret_cast<uint32_t*>(at<uint64_t>(ws, L.scalars) + 16);
-  HIPCHK(hipMemsetAsync(gwide, streams ? 0 : 1, sizeof(uint32_t), s));
   if (bucket) {
     uint64_t* pay = at<uint64_t>(ws, L.pay_a);  // (the bucket path writes Pay records through `keys`)
     rc = streams ? launch_build_keys<true, true>(cell, gene, tgrid, s, kc, rc2, mito, n, toff, b, pay, nullptr, ent_start,
@@ -641,7 +655,6 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     LAUNCH_SHM_N("gene_emit", n, k_gene_emit, dim3((unsigned)cdiv(n, kEmitTile)), dim3(kBlock),
                (staged ? 3 : 2) * sizeof(uint32_t) * (size_t)L.n_buckets, s, rec->gene, rc2, (const uint16_t*)dflags,
                n, (const uint32_t*)gcur, (const uint32_t*)gtoff, L.n_buckets, (const uint32_t*)gwide, staged, gpay);
-    HIPCHK(hipMemsetAsync(gene_partials, 0, sizeof(int64_t) * SCT_NP * (size_t)plan->n_gene_ids, s));
     LAUNCH_N("gene_reduce", n, k_gene_reduce, dim3((unsigned)L.max_gene_work), dim3(kBlock), s, (const void*)gpay,
            (const int64_t*)gwork, (const int64_t*)n_gwork, plan->n_gene_ids, (const uint32_t*)gwide, gene_partials);
   }

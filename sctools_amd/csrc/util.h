@@ -159,6 +159,46 @@ struct ProfScope {
   } while (0);                                                   \
   LAUNCHCHK()
 
+// Several small fills in one launch (round 5: the step issued ~10 hipMemsetAsync calls, each its
+// own ~5 us kernel).  Span k gets the byte value val[k] (memset semantics); blockIdx.y picks the span,
+// 16-byte stores where the span allows them.
+constexpr int kFillSpans = 10;
+struct FillSpans {
+  uint8_t* p[kFillSpans];
+  uint64_t bytes[kFillSpans];
+  uint32_t val[kFillSpans];
+  int n;
+};
+__global__ void __launch_bounds__(256) k_fill_spans(FillSpans f) {
+  const int k = blockIdx.y;
+  uint8_t* p = f.p[k];
+  const uint64_t nb = f.bytes[k];
+  const uint32_t v8 = f.val[k] & 0xffu;
+  const uint32_t v = v8 * 0x01010101u;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t head = ((16 - ((uintptr_t)p & 15)) & 15) < nb ? ((16 - ((uintptr_t)p & 15)) & 15) : nb;
+  if (i0 < head) p[i0] = (uint8_t)v8;
+  const uint64_t nw = (nb - head) / 16;
+  uint4* q = reinterpret_cast<uint4*>(p + head);
+  for (uint64_t i = i0; i < nw; i += stride) q[i] = make_uint4(v, v, v, v);
+  const uint64_t tail0 = head + nw * 16;
+  if (i0 < nb - tail0) p[tail0 + i0] = (uint8_t)v8;
+}
+struct FillBatch {
+  FillSpans f{};
+  uint64_t most = 0;
+  void add(void* p, size_t bytes, uint8_t val = 0) {
+    if (!bytes) return;
+    f.p[f.n] = static_cast<uint8_t*>(p);
+    f.bytes[f.n] = bytes;
+    f.val[f.n] = val;
+    f.n++;
+    most = bytes > most ? bytes : most;
+  }
+  bool full() const { return f.n == kFillSpans; }
+};
+
 // with `shm` bytes of dynamic LDS (sct_dyn_lds)
 #define LAUNCH_SHM(name, kern, grid, block, shm, strm, ...)        \
   do {                                                             \
@@ -454,4 +494,15 @@ __device__ __forceinline__ void wave_flush_packed16(int32_t (&v)[K], bool member
   }
 }
 
+}  // namespace sct
+
+namespace sct {
+inline int launch_fills(FillBatch& fb, hipStream_t s) {
+  if (!fb.f.n) return SCT_OK;
+  uint64_t blocks = (fb.most / 16 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+  LAUNCH("fill", k_fill_spans, dim3((unsigned)blocks, (unsigned)fb.f.n), dim3(256), s, fb.f);
+  fb = FillBatch{};
+  return SCT_OK;
+}
 }  // namespace sct

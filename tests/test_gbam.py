@@ -302,7 +302,7 @@ def test_parts_decode_matches_host(tmp_path, monkeypatch, n_parts, window):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n_parts,block", [(7, 65280), (12, 30000), (5, 65280)])
+@pytest.mark.parametrize("n_parts,block", [(7, 65280), (12, 30000), (9, 65280)])
 def test_parts_with_empty_parts_match_host(tmp_path, n_parts, block):
     """More parts than record members: some parts own no member and decode no record.
     An empty part starts and lands where the previous part's walk landed (records cross member
