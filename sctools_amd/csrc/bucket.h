@@ -103,10 +103,14 @@ __device__ __forceinline__ Work make_work(uint32_t id, uint32_t start, uint32_t 
   const uint32_t r = start + cnt - b;
   return Work{id, b, r < (uint32_t)kChunk ? r : (uint32_t)kChunk, 0u};
 }
-struct BucketCtl {  // device counters of one level (n_giant, n_big, n_big_rec accumulate over levels)
-  uint32_t n_seg, n_work, n_rec;  // the next level's segments, work items and records
+// Device counters of one level (n_giant and n_big accumulate over levels).  Round 5: no record
+// counters (n_rec, n_big_rec) -- every classify block with a pushed or big child added to them, and
+// those same-line atomics cost level 1's classification 0.09 of its 0.25 ms; the kernels that used
+// them only for their profiling item counts now report none.
+struct BucketCtl {
+  uint32_t n_seg, n_work;  // the next level's segments and work items
   uint32_t n_giant, err;  // err: a mapped ref id >= 2^kRefBits (set by build_keys)
-  uint32_t n_big, n_big_rec;  // big buckets and their records
+  uint32_t n_big;  // big buckets
 };
 
 __device__ __forceinline__ uint64_t payload_w0(uint64_t key, int32_t ref, bool reverse, bool mapped, bool mito) {
@@ -118,11 +122,10 @@ __device__ __forceinline__ uint32_t payload_frag(uint64_t w0) {
   return (uint32_t)(w0 >> 2) & ((1u << kFragBits) - 1);
 }
 
-// ctr: the level's (n_seg, n_work, n_rec) counters
+// ctr: the level's (n_seg, n_work) counters
 __device__ __forceinline__ void push_segment(const Seg& sg, Seg* __restrict__ seg, Work* __restrict__ work,
                                              uint32_t* ctr) {
   const uint32_t id = atomicAdd(&ctr[0], 1u);
-  atomicAdd(&ctr[2], sg.cnt);
   seg[id] = sg;
   const uint32_t nw = (sg.cnt + kChunk - 1) / kChunk;
   const uint32_t w0 = atomicAdd(&ctr[1], nw);
@@ -130,7 +133,7 @@ __device__ __forceinline__ void push_segment(const Seg& sg, Seg* __restrict__ se
 }
 
 // level 0: small entities are terminal buckets, mid-sized ones big buckets; larger ones segments,
-// counted in seg_ctr (n_seg, n_work, n_rec)
+// counted in seg_ctr (n_seg, n_work)
 __global__ void k_bucket_level0(const int64_t* __restrict__ ent_start, int64_t n_ent, int64_t n,
                                 uint16_t* __restrict__ bdesc, uint32_t* __restrict__ bent, Seg* __restrict__ seg,
                                 Work* __restrict__ work, Seg* __restrict__ bigs, BucketCtl* ctl,
@@ -147,7 +150,6 @@ __global__ void k_bucket_level0(const int64_t* __restrict__ ent_start, int64_t n
   }
   if (c <= (uint32_t)kBigCap) {
     bigs[atomicAdd(&ctl->n_big, 1u)] = Seg{(uint32_t)s0, c, (uint32_t)e, 0u};
-    atomicAdd(&ctl->n_big_rec, c);
     return;
   }
   push_segment(Seg{(uint32_t)s0, c, (uint32_t)e, 0u}, seg, work, seg_ctr);
@@ -351,7 +353,6 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
     giants[id] = Seg{start, c, sg.ent, fl | par};
   } else if (big) {
     bigs[atomicAdd(&ctl->n_big, 1u)] = Seg{start, c, sg.ent, fl | par};
-    atomicAdd(&ctl->n_big_rec, c);
   }
   const uint32_t nw = push ? (c + kChunk - 1) / kChunk : 0u;
   // new segments and work items numbered by one scan of (segments << 32 | work items)
@@ -363,7 +364,6 @@ __global__ void __launch_bounds__(kBlock) k_bucket_classify(const Seg* __restric
     s_base[0] = atomicAdd(&ctl->n_seg, (uint32_t)tot_s);
     s_base[1] = atomicAdd(&ctl->n_work, (uint32_t)tot_w);
   }
-  if (push) atomicAdd(&ctl->n_rec, c);  // the new segments' records (a few per block)
   __syncthreads();
   if (push) {
     const uint32_t id = s_base[0] + so;

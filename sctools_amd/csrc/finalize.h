@@ -466,6 +466,156 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
   }
 }
 
+// Round 5: the head groups' chains on three waves of one block (k_welford_head2).  The lone wave of
+// k_welford_chains that carries the longest entity is issue-bound: per record it issues the mean
+// chain (sub, two FMAs, add: 4 dependent FP64 operations), the previous record's M2 term (two subs,
+// mul, add), the sample loads and the selects of lanes past their end -- ~66 cycles per record.  Here
+//   wave 0 (mean)   runs the mean chain alone, per chunk of kW2Chunk records: the chunk's samples read
+//                   from LDS into registers, the means stepped with the same operations as
+//                   k_welford_chains (so the same bits), each record's mean written to LDS.  No
+//                   selects: a lane past its chain's end steps on over repeated samples, unused;
+//   wave 1 (M2)     one chunk behind: per record delta = x - mean_{k-1}, d2 = x - mean_k,
+//                   m2 += delta * d2 (stats.py:82-87: the same roundings in the same order), from the
+//                   staged samples and means; a lane's final mean is taken here at its last record
+//                   (chunks a lane finishes take a slower path with selects; finished lanes sit out);
+//   wave 2 (loader) loads the samples from HBM four chunks ahead into registers and stages them in
+//                   LDS two chunks ahead of the mean wave.
+// The waves meet at one block barrier per chunk.
+constexpr int kW2Chunk = 32;
+constexpr int kW2Waves = 3;
+template <bool kCell>
+__global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_t* __restrict__ ent_start,
+                                                                      int64_t n_ent, int64_t n,
+                                                                      const uint32_t* __restrict__ order,
+                                                                      const WelfordCtl* __restrict__ ctl_head,
+                                                                      const double* __restrict__ xs,
+                                                                      double* __restrict__ out_f) {
+  constexpr int ns = kCell ? 4 : 3;
+  constexpr int C = kW2Chunk;
+  __shared__ double s_x[4][C][kWave];  // samples: chunk j in slot j & 3
+  __shared__ double s_m[2][C][kWave];  // means: chunk j in slot j & 1
+  const int lane = threadIdx.x & (kWave - 1);
+  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));  // 0 mean, 1 M2, 2 loader
+  const int st = lane & 3;
+  const uint32_t n_big = ctl_head->n_big;
+  if (blockIdx.x * (uint32_t)kWfGroup >= n_big) return;  // block-uniform
+  const uint32_t k = blockIdx.x * (uint32_t)kWfGroup + (uint32_t)(lane >> 2);
+  const bool mine = k < n_big && st < ns;
+  int64_t e = 0, s = 0, len = 0;
+  if (mine) {
+    e = order[k];
+    s = ent_start[e];
+    len = ent_end(ent_start, e, n_ent, n) - s;
+  }
+  int64_t kmax = len;  // the group's longest chain (the same in every wave)
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    const int64_t o = __shfl_xor(kmax, off);
+    kmax = o > kmax ? o : kmax;
+  }
+  const int64_t clen = mine ? len : kmax;  // a lane without a chain steps along, its result unused
+  const int64_t lastx = clen > 0 ? clen - 1 : 0;
+  const double* X = xs + 4 * s + st;
+  const int64_t P = (kmax + C - 1) / C;
+  double rb[2][C];  // loader: chunk j in flight in rb[j & 1]; mean wave: the current chunk's samples in rb[0]
+  const auto load = [&](double(&b)[C], int64_t j) {
+#pragma unroll
+    for (int q = 0; q < C; q++) {
+      const int64_t kq = j * C + q;
+      b[q] = X[4 * (kq < lastx ? kq : lastx)];
+    }
+  };
+  const auto stage = [&](const double(&b)[C], int64_t j) {
+#pragma unroll
+    for (int q = 0; q < C; q++) s_x[j & 3][q][lane] = b[q];
+  };
+  double mean = 0.0;                        // mean wave
+  double m2 = 0.0, mprev = 0.0, fin = 0.0;  // M2 wave
+  if (role == 2) {
+    load(rb[0], 0);
+    if (P > 1) load(rb[1], 1);
+    stage(rb[0], 0);
+    if (P > 1) stage(rb[1], 1);
+    if (P > 2) load(rb[0], 2);
+    if (P > 3) load(rb[1], 3);
+  }
+  __syncthreads();
+  const auto phase = [&](int64_t p, auto par) {
+    constexpr int pb = decltype(par)::value;  // p & 1 (the loader's register buffer)
+    if (role == 0) {
+      if (p < P) {
+        const int xs_slot = (int)(p & 3), ms_slot = (int)(p & 1);
+#pragma unroll
+        for (int q = 0; q < C; q++) rb[0][q] = s_x[xs_slot][q][lane];
+        const int64_t c = p * C;
+        double yh16 = 0.0, yl16 = 0.0;
+#pragma unroll
+        for (int q = 0; q < C; q++) {
+          if ((q & 15) == 0) {  // each row's lane j: the pair of record c + q + j
+            const double kq = (double)(c + q + (lane & 15) + 1);
+            yh16 = 1.0 / kq;
+            yl16 = __fma_rn(-kq, yh16, 1.0) * yh16;
+          }
+          const double delta = rb[0][q] - mean;
+          double t = 0.0;
+          fmac_row_bcast(t, yl16, delta, q & 15);  // RN(l delta)
+          fmac_row_bcast(t, yh16, delta, q & 15);  // RN(h delta + RN(l delta)) = RN(delta / k)
+          mean = mean + t;
+          s_m[ms_slot][q][lane] = mean;
+        }
+      }
+    } else if (role == 1) {
+      if (p >= 1) {
+        const int64_t c = (p - 1) * C;
+        const int xs_slot = (int)((p - 1) & 3), ms_slot = (int)((p - 1) & 1);
+        const bool full = c + C < clen, part = c < clen && !full;  // part: the lane's last record is in it
+        if (__builtin_amdgcn_ballot_w64(part) != 0) {  // some lane's chain ends in this chunk
+#pragma unroll
+          for (int q = 0; q < C; q++) {
+            const double x = s_x[xs_slot][q][lane];
+            const double mnew = s_m[ms_slot][q][lane];
+            const double delta = x - mprev;
+            const double d2 = x - mnew;
+            const double p2 = delta * d2;
+            m2 = (c + q < clen) ? m2 + p2 : m2;
+            fin = (c + q == clen - 1) ? mnew : fin;
+            mprev = mnew;
+          }
+        } else if (full) {  // (lanes already past their end sit out)
+#pragma unroll
+          for (int q = 0; q < C; q++) {
+            const double x = s_x[xs_slot][q][lane];
+            const double mnew = s_m[ms_slot][q][lane];
+            const double delta = x - mprev;
+            const double d2 = x - mnew;
+            m2 = m2 + delta * d2;
+            mprev = mnew;
+          }
+        }
+      }
+    } else {
+      if (p + 2 < P) {
+        stage(rb[pb], p + 2);  // chunk p + 2, loaded two phases ago (its slot's chunk p - 2 is done)
+        if (p + 4 < P) load(rb[pb], p + 4);
+      }
+    }
+    __syncthreads();
+  };
+  for (int64_t p = 0; p <= P; p += 2) {
+    phase(p, std::integral_constant<int, 0>{});
+    if (p + 1 <= P) phase(p + 1, std::integral_constant<int, 1>{});
+  }
+  if (role != 1 || !mine) return;
+  double* F = out_f + e * SCT_NF;
+  const int mslot = st == 0 ? SCT_F_UY_MEAN : st == 1 ? SCT_F_GQF_MEAN : st == 2 ? SCT_F_GQ_MEAN : SCT_F_CY_MEAN;
+  const int vslot = st == 0 ? SCT_F_UY_VAR : st == 1 ? SCT_F_GQF_VAR : st == 2 ? SCT_F_GQ_VAR : SCT_F_CY_VAR;
+  F[mslot] = fin;
+  F[vslot] = len < 2 ? __builtin_nan("") : m2 / ((double)len - 1.0);
+  if (!kCell && st == 0) {
+    F[SCT_F_CY_MEAN] = 0.0;
+    F[SCT_F_CY_VAR] = 0.0;
+  }
+}
+
 // Entities of < kWfWave records: one lane each (the big ones are left to k_welford_wave).
 template <bool kCell>
 __global__ void k_welford(RecCols r, const int64_t* __restrict__ ent_start, int64_t n_ent, int64_t n,

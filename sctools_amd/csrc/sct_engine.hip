@@ -268,7 +268,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   } else {
     HIPCHK(hipMemsetAsync(bdesc, 0, sizeof(uint16_t) * (size_t)n, s));
     HIPCHK(hipMemsetAsync(ctl, 0, offsetof(BucketCtl, err), s));  // keeps ctl->err from build_keys
-    HIPCHK(hipMemsetAsync(&ctl->n_big, 0, 2 * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(&ctl->n_big, 0, sizeof(uint32_t), s));
     LAUNCH("bucket_level0", k_bucket_level0, dim3((unsigned)cdiv(n_ent, kBlock)), dim3(kBlock), s, ent_start, n_ent,
            n, bdesc, bent, seg[0], work[0], bigs, ctl, &ctl->n_seg);
   }
@@ -286,16 +286,16 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     const Pay* pin = src ? pb : pa;
     Pay* pout = src ? pa : pb;
     HIPCHK(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kRadix * (size_t)h.n_seg, s));
-    LAUNCH_N("bucket_hist", h.n_rec, k_bucket_hist, dim3(h.n_work), dim3(kBlock), s, pin, (const Seg*)seg[c],
+    LAUNCH("bucket_hist", k_bucket_hist, dim3(h.n_work), dim3(kBlock), s, pin, (const Seg*)seg[c],
            (const Work*)work[c], shift, bits, hist);
-    HIPCHK(hipMemsetAsync(ctl, 0, 3 * sizeof(uint32_t), s));  // next level's n_seg, n_work, n_rec
+    HIPCHK(hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), s));  // next level's n_seg, n_work
     LAUNCH("bucket_classify", k_bucket_classify, dim3(h.n_seg), dim3(kBlock), s, (const Seg*)seg[c], hist, cur, depth,
            bits, b.k1, b.k1 + b.k2, KB, level & 1, 0, bdesc, bent, seg[c ^ 1], work[c ^ 1], giants, bigs, ctl,
            (const uint32_t*)nullptr);
     // the next level's counts are final after classify: read them while the scatter runs
     if (int rb = readback_start(ctl, sizeof(h), s)) return rb;
     const uint32_t n_work = h.n_work;
-    LAUNCH_N("bucket_scatter", h.n_rec, k_bucket_scatter, dim3(n_work), dim3(kSBlock), s, pin, pout,
+    LAUNCH("bucket_scatter", k_bucket_scatter, dim3(n_work), dim3(kSBlock), s, pin, pout,
            (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
     if (int rb = readback_finish(&h, sizeof(h))) return rb;
     c ^= 1;
@@ -316,7 +316,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     const dim3 bgrid(h.n_big);
     const bool wide = b.k1 > kNarrowK1Bits;
 #define SCT_BIG(C, G, W)                                                                                          \
-  LAUNCH_N("big_bucket", h.n_big_rec, (k_big_bucket<C, G, W>), bgrid, dim3(kBigBlock), s, (const Seg*)bigs, pa, pb, b, \
+  LAUNCH("big_bucket", (k_big_bucket<C, G, W>), bgrid, dim3(kBigBlock), s, (const Seg*)bigs, pa, pb, b, \
          partials, dflags)
     if (cell && gene) {
       if (wide) { SCT_BIG(true, true, true); } else { SCT_BIG(true, true, false); }
@@ -438,8 +438,16 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
     if (cell) {
       LAUNCH("welford_x_head", k_welford_x_ents<true>, hgrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n,
              (const uint32_t*)worder, (const WelfordCtl*)wch, xs);
-      LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfHeadGroups), dim3(kBlock), s2, ent_start, n_ent, n,
-               (const uint32_t*)worder, wch, (const double*)xs, out_f);
+#ifndef SCT_WF_HEAD2
+#define SCT_WF_HEAD2 0
+#endif
+      if (SCT_WF_HEAD2) {  // round 5: mean chain, M2 terms and loads on three waves per head group
+        LAUNCH_N("welford_head", n, k_welford_head2<true>, dim3(kWfHeadGroups), dim3(kW2Waves * kWave), s2, ent_start, n_ent,
+                 n, (const uint32_t*)worder, (const WelfordCtl*)wch, (const double*)xs, out_f);
+      } else {
+        LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfHeadGroups), dim3(kBlock), s2, ent_start, n_ent,
+                 n, (const uint32_t*)worder, wch, (const double*)xs, out_f);
+      }
       LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s3, rc2, n, xs, ent_start, n_ent,
                (const uint32_t*)worder, (const uint32_t*)&wch->n_big);
       LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,
@@ -447,8 +455,16 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
     } else {
       LAUNCH("welford_x_head", k_welford_x_ents<false>, hgrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n,
              (const uint32_t*)worder, (const WelfordCtl*)wch, xs);
-      LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfHeadGroups), dim3(kBlock), s2, ent_start, n_ent, n,
-               (const uint32_t*)worder, wch, (const double*)xs, out_f);
+#ifndef SCT_WF_HEAD2
+#define SCT_WF_HEAD2 0
+#endif
+      if (SCT_WF_HEAD2) {  // round 5: mean chain, M2 terms and loads on three waves per head group
+        LAUNCH_N("welford_head", n, k_welford_head2<false>, dim3(kWfHeadGroups), dim3(kW2Waves * kWave), s2, ent_start, n_ent,
+                 n, (const uint32_t*)worder, (const WelfordCtl*)wch, (const double*)xs, out_f);
+      } else {
+        LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfHeadGroups), dim3(kBlock), s2, ent_start, n_ent,
+                 n, (const uint32_t*)worder, wch, (const double*)xs, out_f);
+      }
       LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s3, rc2, n, xs, ent_start, n_ent,
                (const uint32_t*)worder, (const uint32_t*)&wch->n_big);
       LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,

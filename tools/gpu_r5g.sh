@@ -1,0 +1,6 @@
+#!/bin/bash
+# Round 5: where the waves of a small workgroup land (SIMDs), and the Welford head kernels alone on one
+# 272k-record entity.
+set -o pipefail
+timeout -k 10 60 ./tools/debug/hwid || exit 1
+timeout -k 10 120 ./tools/debug/w2 272000 || exit 1
