@@ -467,22 +467,44 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
 }
 
 // Round 5: the head groups' chains on three waves of one block (k_welford_head2).  The lone wave of
-// k_welford_chains that carries the longest entity is issue-bound: per record it issues the mean
-// chain (sub, two FMAs, add: 4 dependent FP64 operations), the previous record's M2 term (two subs,
-// mul, add), the sample loads and the selects of lanes past their end -- ~66 cycles per record.  Here
-//   wave 0 (mean)   runs the mean chain alone, per chunk of kW2Chunk records: the chunk's samples read
-//                   from LDS into registers, the means stepped with the same operations as
-//                   k_welford_chains (so the same bits), each record's mean written to LDS.  No
-//                   selects: a lane past its chain's end steps on over repeated samples, unused;
+// k_welford_chains that carries the longest entity is latency-bound on its mean chain: the record's
+// reciprocal pair reaches the two FMAs as DPP row broadcasts, which lengthen the dependent chain
+// (~66 cycles per record with the M2 terms and loads in its gaps).  Here
+//   wave 0 (mean)   runs the mean chain alone on plain FP64 operations: per chunk of kW2Chunk records
+//                   it reads the chunk's samples and reciprocal pairs from LDS into registers, steps
+//                   the means (delta = x - mean, t = RN(l delta), q = RN(h delta + t), mean += q: the
+//                   operations of k_welford_chains, so the same bits) and writes every mean to LDS.
+//                   No selects: a lane past its chain's end steps on over repeated samples, unused;
 //   wave 1 (M2)     one chunk behind: per record delta = x - mean_{k-1}, d2 = x - mean_k,
-//                   m2 += delta * d2 (stats.py:82-87: the same roundings in the same order), from the
+//                   m2 += delta * d2 (stats.py:82-87: the same roundings in the same order) from the
 //                   staged samples and means; a lane's final mean is taken here at its last record
 //                   (chunks a lane finishes take a slower path with selects; finished lanes sit out);
-//   wave 2 (loader) loads the samples from HBM four chunks ahead into registers and stages them in
-//                   LDS two chunks ahead of the mean wave.
-// The waves meet at one block barrier per chunk.
-constexpr int kW2Chunk = 32;
+//   wave 2 (loader) three chunks ahead, copies the samples HBM -> LDS with direct-to-LDS loads (16 B
+//                   per lane: two records of a group's 16 entities per load, no registers in flight)
+//                   and computes the chunk's reciprocal pairs.
+// The waves meet at one block barrier per chunk (LDS writes done first; the loader also waits for the
+// chunk the next phase reads).
+#ifndef SCT_W2_CHUNK
+#define SCT_W2_CHUNK 16
+#endif
+constexpr int kW2Chunk = SCT_W2_CHUNK;  // records per chunk
+constexpr int kW2Slots = 8;             // LDS sample slots: chunks p - 1 .. p + 3 in use at phase p
 constexpr int kW2Waves = 3;
+static_assert(kW2Chunk % 2 == 0 && kW2Chunk / 2 <= 16, "two records per load; vmcnt counts two chunks' loads");
+// The block barrier of k_welford_head2: LDS writes done, then s_barrier -- without the fence of
+// __syncthreads(), which also waits for every load in flight.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#ifdef SCT_W2_PROF  // experiments (tools/debug/welford_head2_micro.hip): per-wave ticks in barriers and in all
+__device__ unsigned long long sct_w2_prof[2 * 4];
+#define W2_BARRIER()                           \
+  do {                                         \
+    const long long _t = wall_clock64();       \
+    lds_barrier();                             \
+    w2_wait += wall_clock64() - _t;            \
+  } while (0)
+#else
+#define W2_BARRIER() lds_barrier()
+#endif
 template <bool kCell>
 __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_t* __restrict__ ent_start,
                                                                       int64_t n_ent, int64_t n,
@@ -492,118 +514,135 @@ __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_
                                                                       double* __restrict__ out_f) {
   constexpr int ns = kCell ? 4 : 3;
   constexpr int C = kW2Chunk;
-  __shared__ double s_x[4][C][kWave];  // samples: chunk j in slot j & 3
-  __shared__ double s_m[2][C][kWave];  // means: chunk j in slot j & 1
+  __shared__ double s_x[kW2Slots][C][kWave];  // samples: chunk j in slot j % kW2Slots, [record][lane]
+  __shared__ double s_m[2][C][kWave];         // means: chunk j in slot j & 1
+  __shared__ double2 s_y[kW2Slots][C];        // the reciprocal pairs of chunk j's record indices
+#ifdef SCT_W2_PROF
+  long long w2_wait = 0;
+  const long long w2_t0 = wall_clock64();
+#endif
   const int lane = threadIdx.x & (kWave - 1);
   const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));  // 0 mean, 1 M2, 2 loader
   const int st = lane & 3;
   const uint32_t n_big = ctl_head->n_big;
   if (blockIdx.x * (uint32_t)kWfGroup >= n_big) return;  // block-uniform
-  const uint32_t k = blockIdx.x * (uint32_t)kWfGroup + (uint32_t)(lane >> 2);
-  const bool mine = k < n_big && st < ns;
-  int64_t e = 0, s = 0, len = 0;
-  if (mine) {
-    e = order[k];
-    s = ent_start[e];
-    len = ent_end(ent_start, e, n_ent, n) - s;
-  }
+  // the group's entity of this lane's chain (4 lanes per entity, one per stream)
+  const auto entity = [&](int slot, int64_t& e, int64_t& s, int64_t& len) {
+    const uint32_t k = blockIdx.x * (uint32_t)kWfGroup + (uint32_t)slot;
+    e = 0, s = 0, len = 0;
+    if (k < n_big) {
+      e = order[k];
+      s = ent_start[e];
+      len = ent_end(ent_start, e, n_ent, n) - s;
+    }
+  };
+  int64_t e, s, len;
+  entity(lane >> 2, e, s, len);
+  const bool mine = len > 0 && st < ns;
   int64_t kmax = len;  // the group's longest chain (the same in every wave)
   for (int off = kWave / 2; off > 0; off >>= 1) {
     const int64_t o = __shfl_xor(kmax, off);
     kmax = o > kmax ? o : kmax;
   }
   const int64_t clen = mine ? len : kmax;  // a lane without a chain steps along, its result unused
-  const int64_t lastx = clen > 0 ? clen - 1 : 0;
-  const double* X = xs + 4 * s + st;
   const int64_t P = (kmax + C - 1) / C;
-  double rb[2][C];  // loader: chunk j in flight in rb[j & 1]; mean wave: the current chunk's samples in rb[0]
-  const auto load = [&](double(&b)[C], int64_t j) {
-#pragma unroll
-    for (int q = 0; q < C; q++) {
-      const int64_t kq = j * C + q;
-      b[q] = X[4 * (kq < lastx ? kq : lastx)];
-    }
-  };
-  const auto stage = [&](const double(&b)[C], int64_t j) {
-#pragma unroll
-    for (int q = 0; q < C; q++) s_x[j & 3][q][lane] = b[q];
-  };
-  double mean = 0.0;                        // mean wave
-  double m2 = 0.0, mprev = 0.0, fin = 0.0;  // M2 wave
+  double m2 = 0.0, mprev = 0.0, fin = 0.0;  // the M2 wave's results
+  // one loop per role (the waves meet at P + 2 barriers: the prologue's and one per phase 0 .. P)
   if (role == 2) {
-    load(rb[0], 0);
-    if (P > 1) load(rb[1], 1);
-    stage(rb[0], 0);
-    if (P > 1) stage(rb[1], 1);
-    if (P > 2) load(rb[0], 2);
-    if (P > 3) load(rb[1], 3);
-  }
-  __syncthreads();
-  const auto phase = [&](int64_t p, auto par) {
-    constexpr int pb = decltype(par)::value;  // p & 1 (the loader's register buffer)
-    if (role == 0) {
-      if (p < P) {
-        const int xs_slot = (int)(p & 3), ms_slot = (int)(p & 1);
+    // loader lane i moves 16 bytes: streams 2 (i & 1) .. +1 of entity (i & 31) / 2 at record offset i / 32
+    int64_t le, ls, llen;
+    entity((lane & 31) >> 1, le, ls, llen);
+    const int64_t llast = (llen > 0 ? llen : kmax) - 1;
+    const double* LX = xs + 4 * ls + 2 * (lane & 1);
+    const int rofs = lane >> 5;
+    const auto issue = [&](int64_t j) {  // chunk j: C / 2 loads, and its reciprocal pairs
+      const int sl = (int)(j % kW2Slots);
 #pragma unroll
-        for (int q = 0; q < C; q++) rb[0][q] = s_x[xs_slot][q][lane];
-        const int64_t c = p * C;
-        double yh16 = 0.0, yl16 = 0.0;
+      for (int u = 0; u < C / 2; u++) {
+        const int64_t kq = j * C + 2 * u + rofs;
+        __builtin_amdgcn_global_load_lds(LX + 4 * (kq < llast ? kq : llast), &s_x[sl][2 * u][0], 16, 0, 0);
+      }
+      if (lane < C) {  // 1 / k as yh + yl for k = j C + lane + 1 (the pairs k_welford_chains computes)
+        const double kq = (double)(j * C + lane + 1);
+        const double yh = 1.0 / kq;
+        s_y[sl][lane] = make_double2(yh, __fma_rn(-kq, yh, 1.0) * yh);
+      }
+    };
+    issue(0);
+    issue(1);
+    issue(2);
+    asm volatile("s_waitcnt vmcnt(%0)" : : "n"(C) : "memory");  // chunk 0 landed (1 and 2 may be in flight)
+    W2_BARRIER();
+    for (int64_t p = 0; p <= P; p++) {
+      issue(p + 3);
+      asm volatile("s_waitcnt vmcnt(%0)" : : "n"(C) : "memory");  // chunk p + 1 landed
+      W2_BARRIER();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (role == 0) {  // the mean chain, chunk p in phase p
+    W2_BARRIER();
+    double mean = 0.0;
+    for (int64_t p = 0; p < P; p++) {
+      const int xs_slot = (int)(p % kW2Slots), ms_slot = (int)(p & 1);
+      double xv[C];
+      double2 yv[C];
+#pragma unroll
+      for (int q = 0; q < C; q++) {
+        xv[q] = s_x[xs_slot][q][lane];
+        yv[q] = s_y[xs_slot][q];
+      }
+#pragma unroll
+      for (int q = 0; q < C; q++) {
+        const double delta = xv[q] - mean;
+        const double t = yv[q].y * delta;               // RN(l delta)
+        const double qd = __fma_rn(delta, yv[q].x, t);  // RN(h delta + RN(l delta)) = RN(delta / k)
+        mean = mean + qd;
+        s_m[ms_slot][q][lane] = mean;
+      }
+      W2_BARRIER();
+    }
+    W2_BARRIER();  // (phase P: the M2 wave's last chunk)
+  } else {  // the M2 terms, chunk p - 1 in phase p
+    W2_BARRIER();
+    W2_BARRIER();  // (phase 0)
+    for (int64_t p = 1; p <= P; p++) {
+      const int64_t c = (p - 1) * C;
+      const int xs_slot = (int)((p - 1) % kW2Slots), ms_slot = (int)((p - 1) & 1);
+      const bool full = c + C < clen, part = c < clen && !full;  // part: the lane's last record is in it
+      double xb[C], mb[C];  // the chunk's samples and means into registers first
+#pragma unroll
+      for (int q = 0; q < C; q++) {
+        xb[q] = s_x[xs_slot][q][lane];
+        mb[q] = s_m[ms_slot][q][lane];
+      }
+      if (__builtin_amdgcn_ballot_w64(part) != 0) {  // some lane's chain ends in this chunk
 #pragma unroll
         for (int q = 0; q < C; q++) {
-          if ((q & 15) == 0) {  // each row's lane j: the pair of record c + q + j
-            const double kq = (double)(c + q + (lane & 15) + 1);
-            yh16 = 1.0 / kq;
-            yl16 = __fma_rn(-kq, yh16, 1.0) * yh16;
-          }
-          const double delta = rb[0][q] - mean;
-          double t = 0.0;
-          fmac_row_bcast(t, yl16, delta, q & 15);  // RN(l delta)
-          fmac_row_bcast(t, yh16, delta, q & 15);  // RN(h delta + RN(l delta)) = RN(delta / k)
-          mean = mean + t;
-          s_m[ms_slot][q][lane] = mean;
+          const double delta = xb[q] - mprev;
+          const double d2 = xb[q] - mb[q];
+          const double p2 = delta * d2;
+          m2 = (c + q < clen) ? m2 + p2 : m2;
+          fin = (c + q == clen - 1) ? mb[q] : fin;
+          mprev = mb[q];
+        }
+      } else if (full) {  // (lanes already past their end sit out)
+#pragma unroll
+        for (int q = 0; q < C; q++) {
+          const double delta = xb[q] - mprev;
+          const double d2 = xb[q] - mb[q];
+          m2 = m2 + delta * d2;
+          mprev = mb[q];
         }
       }
-    } else if (role == 1) {
-      if (p >= 1) {
-        const int64_t c = (p - 1) * C;
-        const int xs_slot = (int)((p - 1) & 3), ms_slot = (int)((p - 1) & 1);
-        const bool full = c + C < clen, part = c < clen && !full;  // part: the lane's last record is in it
-        if (__builtin_amdgcn_ballot_w64(part) != 0) {  // some lane's chain ends in this chunk
-#pragma unroll
-          for (int q = 0; q < C; q++) {
-            const double x = s_x[xs_slot][q][lane];
-            const double mnew = s_m[ms_slot][q][lane];
-            const double delta = x - mprev;
-            const double d2 = x - mnew;
-            const double p2 = delta * d2;
-            m2 = (c + q < clen) ? m2 + p2 : m2;
-            fin = (c + q == clen - 1) ? mnew : fin;
-            mprev = mnew;
-          }
-        } else if (full) {  // (lanes already past their end sit out)
-#pragma unroll
-          for (int q = 0; q < C; q++) {
-            const double x = s_x[xs_slot][q][lane];
-            const double mnew = s_m[ms_slot][q][lane];
-            const double delta = x - mprev;
-            const double d2 = x - mnew;
-            m2 = m2 + delta * d2;
-            mprev = mnew;
-          }
-        }
-      }
-    } else {
-      if (p + 2 < P) {
-        stage(rb[pb], p + 2);  // chunk p + 2, loaded two phases ago (its slot's chunk p - 2 is done)
-        if (p + 4 < P) load(rb[pb], p + 4);
-      }
+      W2_BARRIER();
     }
-    __syncthreads();
-  };
-  for (int64_t p = 0; p <= P; p += 2) {
-    phase(p, std::integral_constant<int, 0>{});
-    if (p + 1 <= P) phase(p + 1, std::integral_constant<int, 1>{});
   }
+#ifdef SCT_W2_PROF
+  if (lane == 0) {
+    sct_w2_prof[2 * role] = (unsigned long long)w2_wait;
+    sct_w2_prof[2 * role + 1] = (unsigned long long)(wall_clock64() - w2_t0);
+  }
+#endif
   if (role != 1 || !mine) return;
   double* F = out_f + e * SCT_NF;
   const int mslot = st == 0 ? SCT_F_UY_MEAN : st == 1 ? SCT_F_GQF_MEAN : st == 2 ? SCT_F_GQ_MEAN : SCT_F_CY_MEAN;

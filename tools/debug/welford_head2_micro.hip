@@ -65,6 +65,14 @@ int main(int argc, char** argv) {
       memcpy(&u, &ho[i], 8);
       hash[which] = hash[which] * 1000003ull ^ u;
     }
+#ifdef SCT_W2_PROF
+    if (which) {
+      unsigned long long pr[8];
+      hipMemcpyFromSymbol(pr, HIP_SYMBOL(sct_w2_prof), sizeof(pr));
+      for (int w = 0; w < 3; w++)
+        printf("  wave %d: %llu ticks in barriers of %llu (wall clock ticks, 100 MHz)\n", w, pr[2 * w], pr[2 * w + 1]);
+    }
+#endif
     printf("%s n %lld  best %.3f ms  %.2f ns/record  result %016llx\n", which ? "head2 " : "chains", (long long)n,
            best, best * 1e6 / n, hash[which]);
   }

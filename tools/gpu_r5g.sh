@@ -4,3 +4,4 @@
 set -o pipefail
 timeout -k 10 60 ./tools/debug/hwid || exit 1
 timeout -k 10 120 ./tools/debug/w2 272000 || exit 1
+bash tools/gpu_tl_ab.sh r5g_tl tree=tree e1=exp/e1_emitpf.so

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5],
                     help="bench.py's workloads: 2 (default), 4 (125M records, 62.5k lognormal(0, 2) cells), "
                          "5 (100M shuffled records sorted by (CB, UB, GE, query name) inside the step)")
+    ap.add_argument("--welford", action="store_true",
+                    help="the drop-in default instead: cell rows only, Welford float mode (bench's dropin_cell_welford_ms)")
     a = ap.parse_args()
     from sctools_amd import engine as E
     from sctools_amd import synth
@@ -55,6 +57,9 @@ def main():
     mito = torch.from_numpy(data.gene_is_mito).to(dev)
     n_ent = eng.count_entities(cols(), "cell", dims)
     for _ in range(a.reps):
+        if a.welford:
+            eng.compute(cols(), "cell", dims, mito, torch.from_numpy(data.gene_is_multi).to(dev), float_mode="welford", n_entities=n_ent)
+            continue
         ci, cf, part = eng.cell_and_gene(cols(), dims, mito, n_entities=n_ent)
         eng.finalize_partials(part)
     torch.cuda.synchronize()
