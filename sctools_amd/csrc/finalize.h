@@ -101,6 +101,7 @@ struct WelfordCtl {
   uint32_t cursor[kWfBins];
   uint32_t head;
   uint32_t n_big;
+  uint32_t started;  // (the head queue's) head blocks resident so far (k_welford_head2 -> k_wf_gate)
 };
 
 __device__ __forceinline__ int64_t ent_end(const int64_t* __restrict__ ent_start, int64_t e, int64_t n_ent,
@@ -109,32 +110,51 @@ __device__ __forceinline__ int64_t ent_end(const int64_t* __restrict__ ent_start
 }
 
 // big entities counted per log2 size class (wave-aggregated)
-__global__ void k_welford_bins(const int64_t* __restrict__ ent_start, int64_t n_ent, int64_t n,
-                               WelfordCtl* __restrict__ ctl) {
+// (round 5: counted per block in LDS first -- one global atomic per (block, size class) instead of
+// one per entity on 32 addresses: 0.2 ms each at config 4)
+__global__ void __launch_bounds__(kBlock) k_welford_bins(const int64_t* __restrict__ ent_start, int64_t n_ent,
+                                                         int64_t n, WelfordCtl* __restrict__ ctl) {
+  __shared__ uint32_t s_c[kWfBins];
+  if (threadIdx.x < kWfBins) s_c[threadIdx.x] = 0;
+  __syncthreads();
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e >= n_ent) return;
-  const int64_t sz = ent_end(ent_start, e, n_ent, n) - ent_start[e];
-  if (sz < kWfWave) return;
-  atomicAdd(&ctl->count[63 - __clzll((unsigned long long)sz)], 1u);
+  if (e < n_ent) {
+    const int64_t sz = ent_end(ent_start, e, n_ent, n) - ent_start[e];
+    if (sz >= kWfWave) atomicAdd(&s_c[63 - __clzll((unsigned long long)sz)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kWfBins && s_c[threadIdx.x]) atomicAdd(&ctl->count[threadIdx.x], s_c[threadIdx.x]);
 }
 
-// big entity ids into `order`, larger size classes first
-__global__ void k_welford_order(const int64_t* __restrict__ ent_start, int64_t n_ent, int64_t n,
-                                WelfordCtl* __restrict__ ctl, uint32_t* __restrict__ order) {
-  __shared__ uint32_t s_base[kWfBins];
+// big entity ids into `order`, larger size classes first (ranks in LDS, one global range per
+// (block, size class))
+__global__ void __launch_bounds__(kBlock) k_welford_order(const int64_t* __restrict__ ent_start, int64_t n_ent,
+                                                          int64_t n, WelfordCtl* __restrict__ ctl,
+                                                          uint32_t* __restrict__ order) {
+  __shared__ uint32_t s_base[kWfBins], s_c[kWfBins];
   if (threadIdx.x < kWfBins) {
     uint32_t b = 0;
     for (int k = threadIdx.x + 1; k < kWfBins; k++) b += ctl->count[k];
     s_base[threadIdx.x] = b;
+    s_c[threadIdx.x] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) ctl->n_big = b + ctl->count[0];
   }
   __syncthreads();
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e >= n_ent) return;
-  const int64_t sz = ent_end(ent_start, e, n_ent, n) - ent_start[e];
-  if (sz < kWfWave) return;
-  const int bin = 63 - __clzll((unsigned long long)sz);
-  order[s_base[bin] + atomicAdd(&ctl->cursor[bin], 1u)] = (uint32_t)e;
+  int bin = -1;
+  uint32_t rank = 0;
+  if (e < n_ent) {
+    const int64_t sz = ent_end(ent_start, e, n_ent, n) - ent_start[e];
+    if (sz >= kWfWave) {
+      bin = 63 - __clzll((unsigned long long)sz);
+      rank = atomicAdd(&s_c[bin], 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kWfBins && s_c[threadIdx.x])
+    s_base[threadIdx.x] += atomicAdd(&ctl->cursor[threadIdx.x], s_c[threadIdx.x]);
+  __syncthreads();
+  if (bin >= 0) order[s_base[bin] + rank] = (uint32_t)e;
 }
 
 // the stream values of record i: x[0] UY, x[1] genomic fraction, x[2] genomic mean, x[3] CY
@@ -466,10 +486,11 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
   }
 }
 
-// Round 5: the head groups' chains on three waves of one block (k_welford_head2).  The lone wave of
-// k_welford_chains that carries the longest entity is latency-bound on its mean chain: the record's
-// reciprocal pair reaches the two FMAs as DPP row broadcasts, which lengthen the dependent chain
-// (~66 cycles per record with the M2 terms and loads in its gaps).  Here
+// Round 5: the head entities' chains on four waves of one block (k_welford_head2), kW2Ents entities
+// per block.  Inside the pipeline the lone wave of k_welford_chains carrying the longest entity ran
+// 1.7x (config 2) its pace alone: while the concurrent kernels keep HBM busy a load takes many
+// microseconds, and one 32-record batch of prefetch (~1 us of its chain) left it waiting (2.6x
+// beside an HBM copy, 2.4x beside FP64 work on its SIMD, tools/debug/welford_head2_micro.hip).  Here
 //   wave 0 (mean)   runs the mean chain alone on plain FP64 operations: per chunk of kW2Chunk records
 //                   it reads the chunk's samples and reciprocal pairs from LDS into registers, steps
 //                   the means (delta = x - mean, t = RN(l delta), q = RN(h delta + t), mean += q: the
@@ -479,23 +500,43 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
 //                   m2 += delta * d2 (stats.py:82-87: the same roundings in the same order) from the
 //                   staged samples and means; a lane's final mean is taken here at its last record
 //                   (chunks a lane finishes take a slower path with selects; finished lanes sit out);
-//   wave 2 (loader) three chunks ahead, copies the samples HBM -> LDS with direct-to-LDS loads (16 B
-//                   per lane: two records of a group's 16 entities per load, no registers in flight)
-//                   and computes the chunk's reciprocal pairs.
-// The waves meet at one block barrier per chunk (LDS writes done first; the loader also waits for the
-// chunk the next phase reads).
+//   waves 2, 3      the loaders, kW2Depth chunks (~1000 records, ~27 us of the chain) ahead, copy the
+//   (loaders)       samples HBM -> LDS with direct-to-LDS loads (16 B per lane, 32 / kW2Ents records of
+//                   the block's entities per load, no registers in flight; each loader holds <= 60
+//                   loads in flight, below vmcnt's 63) and compute the chunk's reciprocal pairs;
+//                   loader w takes the chunks j with j % 2 == w.
+// Few entities per block keep the bytes per chain step small, so the LDS ring reaches far ahead.  The
+// waves meet at one block barrier per chunk (LDS writes done first; the loader of the chunk the next
+// phase reads waits for it).
 #ifndef SCT_W2_CHUNK
 #define SCT_W2_CHUNK 16
 #endif
-constexpr int kW2Chunk = SCT_W2_CHUNK;  // records per chunk
-constexpr int kW2Slots = 8;             // LDS sample slots: chunks p - 1 .. p + 3 in use at phase p
-constexpr int kW2Waves = 3;
-static_assert(kW2Chunk % 2 == 0 && kW2Chunk / 2 <= 16, "two records per load; vmcnt counts two chunks' loads");
+#ifndef SCT_W2_ENTS
+#define SCT_W2_ENTS 16
+#endif
+constexpr int kW2Chunk = SCT_W2_CHUNK;         // records per chunk
+constexpr int kW2Ents = SCT_W2_ENTS;           // entities per block
+constexpr int kW2Lanes = 4 * kW2Ents;          // chain lanes (4 streams per entity)
+constexpr int kW2PerLoad = 32 / kW2Ents;       // records per 64 x 16-byte load
+constexpr int kW2Loads = kW2Chunk / kW2PerLoad;  // loads per chunk
+constexpr int kW2Slots = 64 * 16 / kW2Chunk * 4 / kW2Ents;  // ~128 KB of samples
+constexpr int kW2Depth = (kW2Slots - 2) & ~1;  // chunks in flight ahead of the mean chain
+#ifndef SCT_W2_FILL
+#define SCT_W2_FILL 12
+#endif
+constexpr int kW2Work = 4;                     // mean, M2, two loaders
+constexpr int kW2Waves = kW2Work + SCT_W2_FILL;  // + waves that only hold the CU (see below)
+static_assert(kW2Ents >= 1 && kW2Ents <= 16 && (kW2Ents & (kW2Ents - 1)) == 0, "entities per block: power of 2");
+static_assert(kW2Chunk % kW2PerLoad == 0 && kWfHeadEnts % kW2Ents == 0, "whole loads per chunk, whole blocks");
+static_assert((kW2Slots & (kW2Slots - 1)) == 0 && kW2Slots >= kW2Depth + 2, "slots: chunks p - 1 .. p + depth");
+constexpr int kW2InFlight = (kW2Depth / 2) * kW2Loads;  // a loader's loads in flight after issuing
+constexpr int kW2After = (kW2Depth / 2 - 1) * kW2Loads;  // ... after its chunk the next phase reads
+static_assert(kW2InFlight <= 63, "a loader's loads in flight fit vmcnt");
 // The block barrier of k_welford_head2: LDS writes done, then s_barrier -- without the fence of
 // __syncthreads(), which also waits for every load in flight.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 #ifdef SCT_W2_PROF  // experiments (tools/debug/welford_head2_micro.hip): per-wave ticks in barriers and in all
-__device__ unsigned long long sct_w2_prof[2 * 4];
+__device__ unsigned long long sct_w2_prof[2 * 4 + 2];
 #define W2_BARRIER()                           \
   do {                                         \
     const long long _t = wall_clock64();       \
@@ -509,26 +550,29 @@ template <bool kCell>
 __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_t* __restrict__ ent_start,
                                                                       int64_t n_ent, int64_t n,
                                                                       const uint32_t* __restrict__ order,
-                                                                      const WelfordCtl* __restrict__ ctl_head,
+                                                                      WelfordCtl* __restrict__ ctl_head,
                                                                       const double* __restrict__ xs,
                                                                       double* __restrict__ out_f) {
   constexpr int ns = kCell ? 4 : 3;
   constexpr int C = kW2Chunk;
-  __shared__ double s_x[kW2Slots][C][kWave];  // samples: chunk j in slot j % kW2Slots, [record][lane]
-  __shared__ double s_m[2][C][kWave];         // means: chunk j in slot j & 1
-  __shared__ double2 s_y[kW2Slots][C];        // the reciprocal pairs of chunk j's record indices
+  __shared__ double s_x[kW2Slots][C][kW2Lanes];  // samples: chunk j in slot j % kW2Slots, [record][lane]
+  __shared__ double s_m[2][C][kW2Lanes];         // means: chunk j in slot j & 1
+  __shared__ double2 s_y[kW2Slots][C];           // the reciprocal pairs of chunk j's record indices
 #ifdef SCT_W2_PROF
   long long w2_wait = 0;
   const long long w2_t0 = wall_clock64();
+  const long long w2_c0 = clock64();
 #endif
   const int lane = threadIdx.x & (kWave - 1);
-  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));  // 0 mean, 1 M2, 2 loader
+  const int cl = lane & (kW2Lanes - 1);  // the chain lane this lane mirrors (lanes >= kW2Lanes: copies)
+  const int role = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));  // 0 mean, 1 M2, 2-3 loaders
   const int st = lane & 3;
+  if (threadIdx.x == 0) atomicAdd(&ctl_head->started, 1u);  // resident (k_wf_gate)
   const uint32_t n_big = ctl_head->n_big;
-  if (blockIdx.x * (uint32_t)kWfGroup >= n_big) return;  // block-uniform
-  // the group's entity of this lane's chain (4 lanes per entity, one per stream)
+  if (blockIdx.x * (uint32_t)kW2Ents >= n_big) return;  // block-uniform
+  // the block's entity `slot` (4 lanes per entity, one per stream)
   const auto entity = [&](int slot, int64_t& e, int64_t& s, int64_t& len) {
-    const uint32_t k = blockIdx.x * (uint32_t)kWfGroup + (uint32_t)slot;
+    const uint32_t k = blockIdx.x * (uint32_t)kW2Ents + (uint32_t)slot;
     e = 0, s = 0, len = 0;
     if (k < n_big) {
       e = order[k];
@@ -537,9 +581,9 @@ __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_
     }
   };
   int64_t e, s, len;
-  entity(lane >> 2, e, s, len);
-  const bool mine = len > 0 && st < ns;
-  int64_t kmax = len;  // the group's longest chain (the same in every wave)
+  entity(cl >> 2, e, s, len);
+  const bool mine = lane < kW2Lanes && len > 0 && st < ns;
+  int64_t kmax = len;  // the block's longest chain (the same in every wave)
   for (int off = kWave / 2; off > 0; off >>= 1) {
     const int64_t o = __shfl_xor(kmax, off);
     kmax = o > kmax ? o : kmax;
@@ -548,19 +592,27 @@ __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_
   const int64_t P = (kmax + C - 1) / C;
   double m2 = 0.0, mprev = 0.0, fin = 0.0;  // the M2 wave's results
   // one loop per role (the waves meet at P + 2 barriers: the prologue's and one per phase 0 .. P)
-  if (role == 2) {
-    // loader lane i moves 16 bytes: streams 2 (i & 1) .. +1 of entity (i & 31) / 2 at record offset i / 32
+  if (role >= kW2Work) {
+    // The block's other waves do nothing but meet the barriers: with them the block holds every
+    // SIMD's registers (4 waves x 128 VGPRs each), so no wave of another kernel shares the CU.  The
+    // LDS alone does not ensure it: kernels without LDS (the other chains, the fills) landed beside
+    // the chain and their FP64 work delayed its operations.
+    for (int64_t p = 0; p <= P + 1; p++) W2_BARRIER();
+  } else if (role >= 2) {
+    // loader lane i moves 16 bytes: streams 2 (i & 1) .. +1 of entity (i / 2) % kW2Ents, at record
+    // offset i / (2 kW2Ents) of the load's kW2PerLoad records (LDS row = kW2Lanes doubles)
+    const int w = role - 2;
     int64_t le, ls, llen;
-    entity((lane & 31) >> 1, le, ls, llen);
+    entity((lane >> 1) & (kW2Ents - 1), le, ls, llen);
     const int64_t llast = (llen > 0 ? llen : kmax) - 1;
     const double* LX = xs + 4 * ls + 2 * (lane & 1);
-    const int rofs = lane >> 5;
-    const auto issue = [&](int64_t j) {  // chunk j: C / 2 loads, and its reciprocal pairs
-      const int sl = (int)(j % kW2Slots);
+    const int rofs = lane / (2 * kW2Ents);
+    const auto issue = [&](int64_t j) {  // chunk j: kW2Loads loads, and its reciprocal pairs
+      const int sl = (int)(j & (kW2Slots - 1));
 #pragma unroll
-      for (int u = 0; u < C / 2; u++) {
-        const int64_t kq = j * C + 2 * u + rofs;
-        __builtin_amdgcn_global_load_lds(LX + 4 * (kq < llast ? kq : llast), &s_x[sl][2 * u][0], 16, 0, 0);
+      for (int u = 0; u < kW2Loads; u++) {
+        const int64_t kq = j * C + u * kW2PerLoad + rofs;
+        __builtin_amdgcn_global_load_lds(LX + 4 * (kq < llast ? kq : llast), &s_x[sl][u * kW2PerLoad][0], 16, 0, 0);
       }
       if (lane < C) {  // 1 / k as yh + yl for k = j C + lane + 1 (the pairs k_welford_chains computes)
         const double kq = (double)(j * C + lane + 1);
@@ -568,27 +620,25 @@ __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_
         s_y[sl][lane] = make_double2(yh, __fma_rn(-kq, yh, 1.0) * yh);
       }
     };
-    issue(0);
-    issue(1);
-    issue(2);
-    asm volatile("s_waitcnt vmcnt(%0)" : : "n"(C) : "memory");  // chunk 0 landed (1 and 2 may be in flight)
+    for (int j = w; j < kW2Depth; j += 2) issue(j);
+    if (w == 0) asm volatile("s_waitcnt vmcnt(%0)" : : "n"(kW2After) : "memory");  // chunk 0 landed
     W2_BARRIER();
     for (int64_t p = 0; p <= P; p++) {
-      issue(p + 3);
-      asm volatile("s_waitcnt vmcnt(%0)" : : "n"(C) : "memory");  // chunk p + 1 landed
+      if ((int)(p & 1) == w) issue(p + kW2Depth);                                   // its chunk p was waited for
+      else asm volatile("s_waitcnt vmcnt(%0)" : : "n"(kW2After) : "memory");  // chunk p + 1 landed
       W2_BARRIER();
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load may land in LDS after the block ends
   } else if (role == 0) {  // the mean chain, chunk p in phase p
     W2_BARRIER();
     double mean = 0.0;
     for (int64_t p = 0; p < P; p++) {
-      const int xs_slot = (int)(p % kW2Slots), ms_slot = (int)(p & 1);
+      const int xs_slot = (int)(p & (kW2Slots - 1)), ms_slot = (int)(p & 1);
       double xv[C];
       double2 yv[C];
 #pragma unroll
       for (int q = 0; q < C; q++) {
-        xv[q] = s_x[xs_slot][q][lane];
+        xv[q] = s_x[xs_slot][q][cl];
         yv[q] = s_y[xs_slot][q];
       }
 #pragma unroll
@@ -597,7 +647,7 @@ __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_
         const double t = yv[q].y * delta;               // RN(l delta)
         const double qd = __fma_rn(delta, yv[q].x, t);  // RN(h delta + RN(l delta)) = RN(delta / k)
         mean = mean + qd;
-        s_m[ms_slot][q][lane] = mean;
+        if (lane < kW2Lanes) s_m[ms_slot][q][cl] = mean;
       }
       W2_BARRIER();
     }
@@ -607,13 +657,13 @@ __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_
     W2_BARRIER();  // (phase 0)
     for (int64_t p = 1; p <= P; p++) {
       const int64_t c = (p - 1) * C;
-      const int xs_slot = (int)((p - 1) % kW2Slots), ms_slot = (int)((p - 1) & 1);
+      const int xs_slot = (int)((p - 1) & (kW2Slots - 1)), ms_slot = (int)((p - 1) & 1);
       const bool full = c + C < clen, part = c < clen && !full;  // part: the lane's last record is in it
       double xb[C], mb[C];  // the chunk's samples and means into registers first
 #pragma unroll
       for (int q = 0; q < C; q++) {
-        xb[q] = s_x[xs_slot][q][lane];
-        mb[q] = s_m[ms_slot][q][lane];
+        xb[q] = s_x[xs_slot][q][cl];
+        mb[q] = s_m[ms_slot][q][cl];
       }
       if (__builtin_amdgcn_ballot_w64(part) != 0) {  // some lane's chain ends in this chunk
 #pragma unroll
@@ -638,9 +688,10 @@ __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_
     }
   }
 #ifdef SCT_W2_PROF
-  if (lane == 0) {
+  if (lane == 0 && role < kW2Work) {
     sct_w2_prof[2 * role] = (unsigned long long)w2_wait;
     sct_w2_prof[2 * role + 1] = (unsigned long long)(wall_clock64() - w2_t0);
+    if (role == 0) sct_w2_prof[8] = (unsigned long long)(clock64() - w2_c0);
   }
 #endif
   if (role != 1 || !mine) return;
@@ -653,6 +704,16 @@ __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_
     F[SCT_F_CY_MEAN] = 0.0;
     F[SCT_F_CY_VAR] = 0.0;
   }
+}
+
+// Waits until `want` head blocks are resident (*started, k_welford_head2) or ~kWfGateTicks of the
+// 100 MHz wall clock have passed, whichever is first (a scheduling aid: see welford_stage).
+constexpr int64_t kWfGateTicks = 400000;  // 4 ms
+__global__ void __launch_bounds__(kWave) k_wf_gate(const uint32_t* started, uint32_t want, int64_t max_ticks) {
+  const int64_t t0 = wall_clock64();
+  while (__hip_atomic_load(started + (threadIdx.x & kWave), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want &&
+         wall_clock64() - t0 < max_ticks)
+    __builtin_amdgcn_s_sleep(4);
 }
 
 // Entities of < kWfWave records: one lane each (the big ones are left to k_welford_wave).

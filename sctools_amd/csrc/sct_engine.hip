@@ -435,19 +435,21 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
     double* xs = at<double>(ws, L.wx);
     const dim3 xgrid((unsigned)cdiv(n, kBlock));
     const dim3 hgrid((unsigned)kWfBlocks);
+    // Round 5: the head kernel's blocks each need a whole CU (k_welford_head2), which a flood of
+    // other blocks keeps from them: inside the pipeline its blocks started ~1.4 ms after the launch
+    // (config 2).  The key pass (the caller's stream) and the sample pass (s3) first wait on the
+    // device, boundedly, for the head blocks to be resident (k_wf_gate).  A scheduling aid only: on
+    // the time-out they go on, and nothing waits on them.
+    const uint32_t* started = &wch->started;
+    constexpr unsigned kHeadBlocks = (unsigned)(kWfHeadEnts / kW2Ents);
+    HIPCHK(hipStreamWaitEvent(s, wf.fork3, 0));
+    LAUNCH("welford_gate", k_wf_gate, dim3(1), dim3(kWave), s, started, kHeadBlocks, kWfGateTicks);
+    LAUNCH("welford_gate", k_wf_gate, dim3(1), dim3(kWave), s3, started, kHeadBlocks, kWfGateTicks);
     if (cell) {
       LAUNCH("welford_x_head", k_welford_x_ents<true>, hgrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n,
              (const uint32_t*)worder, (const WelfordCtl*)wch, xs);
-#ifndef SCT_WF_HEAD2
-#define SCT_WF_HEAD2 0
-#endif
-      if (SCT_WF_HEAD2) {  // round 5: mean chain, M2 terms and loads on three waves per head group
-        LAUNCH_N("welford_head", n, k_welford_head2<true>, dim3(kWfHeadGroups), dim3(kW2Waves * kWave), s2, ent_start, n_ent,
-                 n, (const uint32_t*)worder, (const WelfordCtl*)wch, (const double*)xs, out_f);
-      } else {
-        LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfHeadGroups), dim3(kBlock), s2, ent_start, n_ent,
-                 n, (const uint32_t*)worder, wch, (const double*)xs, out_f);
-      }
+      LAUNCH_N("welford_head", n, k_welford_head2<true>, dim3(kHeadBlocks), dim3(kW2Waves * kWave), s2, ent_start,
+               n_ent, n, (const uint32_t*)worder, wch, (const double*)xs, out_f);
       LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s3, rc2, n, xs, ent_start, n_ent,
                (const uint32_t*)worder, (const uint32_t*)&wch->n_big);
       LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,
@@ -455,16 +457,8 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
     } else {
       LAUNCH("welford_x_head", k_welford_x_ents<false>, hgrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n,
              (const uint32_t*)worder, (const WelfordCtl*)wch, xs);
-#ifndef SCT_WF_HEAD2
-#define SCT_WF_HEAD2 0
-#endif
-      if (SCT_WF_HEAD2) {  // round 5: mean chain, M2 terms and loads on three waves per head group
-        LAUNCH_N("welford_head", n, k_welford_head2<false>, dim3(kWfHeadGroups), dim3(kW2Waves * kWave), s2, ent_start, n_ent,
-                 n, (const uint32_t*)worder, (const WelfordCtl*)wch, (const double*)xs, out_f);
-      } else {
-        LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfHeadGroups), dim3(kBlock), s2, ent_start, n_ent,
-                 n, (const uint32_t*)worder, wch, (const double*)xs, out_f);
-      }
+      LAUNCH_N("welford_head", n, k_welford_head2<false>, dim3(kHeadBlocks), dim3(kW2Waves * kWave), s2, ent_start,
+               n_ent, n, (const uint32_t*)worder, wch, (const double*)xs, out_f);
       LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s3, rc2, n, xs, ent_start, n_ent,
                (const uint32_t*)worder, (const uint32_t*)&wch->n_big);
       LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,
@@ -1282,5 +1276,11 @@ int sct_finalize_partials(int32_t mode, const int64_t* partials, int64_t rows, i
          (const int64_t*)nullptr, out_ints, out_floats);
   return SCT_OK;
 }
+
+#ifdef SCT_W2_PROF  // experiments only: the Welford head kernel's per-wave barrier ticks (finalize.h)
+int sct_debug_w2_prof(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(sct_w2_prof), sizeof(sct_w2_prof)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // extern "C"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: the three-wave Welford head kernel with an LDS-only block barrier, chunks of 16 / 32 records,
-# alone on one 272k-record entity against k_welford_chains.
+# Round 5: k_welford_chains against the three-wave head kernel on one 272k-record entity, alone (0),
+# beside an HBM copy (1) and beside FP64 FMA chains on every SIMD (2).
 set -o pipefail
-for c in 16; do timeout -k 10 120 ./tools/debug/w2_$c 272000 || exit 1; done
+for h in 0 1 2; do echo "== background $h"; timeout -k 10 120 ./tools/debug/w2_16 272000 256 $h || exit 1; done
