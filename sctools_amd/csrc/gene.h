@@ -418,14 +418,6 @@ struct GeneFmt<true> {  // gene_payload8; counted bits: 0 PERFECT, 1-2 the xf co
 };
 static_assert(kGeneFlags == 14, "flag bits 14 and 15 are the SECOND events");
 
-// Bit i of an 8-bit value moved to bit 8i (byte i) of a 64-bit word.
-__device__ __forceinline__ uint64_t spread_bytes(uint32_t x) {
-  uint64_t v = x;
-  v = (v | (v << 28)) & 0x0000000F0000000Full;
-  v = (v | (v << 14)) & 0x0003000300030003ull;
-  return (v | (v << 7)) & 0x0101010101010101ull;
-}
-
 // The uy stream's exact-lane increments for one denominator (barcode lengths are fixed in a
 // chemistry): entry a holds fx_increments(RN(a / B)), computed as the other samples are, so a
 // table hit adds the same 8 words the arithmetic would.
@@ -445,22 +437,32 @@ __device__ __forceinline__ void fill_uy_tab(uint32_t B, uint4* tab) {
 // A thread's open run of one gene.  The 16 counted flag bits are counted in bytes of pk (a run
 // stays open over the sub-tiles of one work item, and is flushed before it could reach
 // kRunCap payloads), two 64-bit adds per payload instead of one extract-and-add per flag.
+// Round 5: a payload's 16 flag bits reach the byte counters as four nibbles, each spread to four
+// bytes by a 16-entry LDS table (one 32-bit read and add per nibble, in place of two 64-bit
+// shift-or-mask spreads): 0.891 -> 0.886 ms at config 2, 1.069 -> 1.052 at config 4.  (A gq_gt30
+// increment table like uy's, its 3.2 KB of LDS taken from the sort buffer to keep 3 blocks per CU,
+// was slower: 0.999 ms.  The reduce is not VALU-bound: profiles/r05/gene_reduce/.)
+__device__ __forceinline__ void fill_nib_tab(uint32_t* tab) {
+  const uint32_t v = threadIdx.x;
+  if (v < 16) tab[v] = (v & 1u) | ((v >> 1) & 1u) << 8 | ((v >> 2) & 1u) << 16 | ((v >> 3) & 1u) << 24;
+}
 struct GeneAcc {
-  uint64_t pk[2];  // byte f of pk[f / 8]: #payloads with counted bit f
+  uint32_t pk[4];  // byte f % 4 of pk[f / 4]: #payloads with counted bit f
   int32_t n;       // n_reads
   int64_t l[3 * kStreamLanes];
   __device__ __forceinline__ void clear() {
-    pk[0] = pk[1] = 0;
+    pk[0] = pk[1] = pk[2] = pk[3] = 0;
     n = 0;
 #pragma unroll
     for (int i = 0; i < 3 * kStreamLanes; i++) l[i] = 0;
   }
   // uy_tab: the uy lane increments of a = 0 .. kUyTab - 1 over the work item's uy denominator uy_b
   // (kNoUyTab: none); other denominators are computed
-  __device__ __forceinline__ void add(const GeneItem& g, const double* s_rcp, const uint4* uy_tab, uint32_t uy_b) {
+  __device__ __forceinline__ void add(const GeneItem& g, const double* s_rcp, const uint4* uy_tab, uint32_t uy_b,
+                                      const uint32_t* nib) {
     n += 1;
-    pk[0] += spread_bytes(g.f & 0xffu);
-    pk[1] += spread_bytes(g.f >> 8);
+#pragma unroll
+    for (int j = 0; j < 4; j++) pk[j] += nib[(g.f >> (4 * j)) & 15u];
     if (g.ub == uy_b && g.ua <= uy_b) {
       const uint4 i0 = uy_tab[2 * g.ua], i1 = uy_tab[2 * g.ua + 1];
       l[0] += i0.x, l[1] += i0.y, l[2] += i0.z, l[3] += i0.w;
@@ -472,7 +474,7 @@ struct GeneAcc {
     fx_accumulate(l + 1 * kStreamLanes, ratio_y(g.qa, g.qb, yq));
     fx_accumulate(l + 2 * kStreamLanes, ratio_y(g.qs, g.qb, yq));
   }
-  __device__ __forceinline__ int32_t byte(int f) const { return (int32_t)((pk[f / 8] >> (8 * (f % 8))) & 0xffu); }
+  __device__ __forceinline__ int32_t byte(int f) const { return (int32_t)((pk[f / 4] >> (8 * (f % 4))) & 0xffu); }
   // unconditional adds (zeros included): a per-lane test would cost an exec-mask round per lane
   template <bool k8>
   __device__ __forceinline__ void flush(int32_t* cbin, unsigned long long* lbin) const {
@@ -538,8 +540,8 @@ __device__ __forceinline__ void gene_wave_flush(GeneAcc& acc, int key, int32_t* 
   uint32_t c[kGenePack];
 #pragma unroll
   for (int j = 0; j < 8; j++) {
-    const uint64_t w = acc.pk[j / 4] >> (16 * (j % 4));
-    c[j] = (uint32_t)(w & 0xffu) | ((uint32_t)((w >> 8) & 0xffu) << 16);
+    const uint32_t w = acc.pk[j / 2] >> (16 * (j % 2));
+    c[j] = (w & 0xffu) | (((w >> 8) & 0xffu) << 16);
   }
   c[8] = (uint32_t)acc.n;
   if (__ballot(m0)) seg_step<0x111, 0xf>(c, acc.l, m0);  // row_shr:1
@@ -574,7 +576,7 @@ template <bool k8>
 __device__ __forceinline__ void gene_reduce_item(const void* __restrict__ pay, int64_t beg, int64_t end, uint32_t g0,
                                                  uint4* s_buf, int32_t* s_cbin, unsigned long long* s_lbin,
                                                  uint32_t* s_cnt, uint32_t* s_start, uint64_t* s_scan,
-                                                 const double* s_rcp, uint4* s_uytab) {
+                                                 const double* s_rcp, uint4* s_uytab, const uint32_t* s_nib) {
   using F = GeneFmt<k8>;
   using W = typename F::W;
   constexpr int kSub = F::kSub, kItems = kSub / kBlock;
@@ -648,7 +650,7 @@ __device__ __forceinline__ void gene_reduce_item(const void* __restrict__ pay, i
         acc.clear();
         cur = (int)g.lg;
       }
-      acc.add(g, s_rcp, s_uytab, uy_b);
+      acc.add(g, s_rcp, s_uytab, uy_b, s_nib);
     }
     __syncthreads();  // s_sorted / s_cnt are reused by the next sub-tile
   }
@@ -670,9 +672,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
   __shared__ uint64_t s_scan[kWaves + 1];
   __shared__ double s_rcp[kRcpN];
   __shared__ uint4 s_uytab[2 * kUyTab];
+  __shared__ uint32_t s_nib[16];
   if ((int64_t)blockIdx.x >= *n_work) return;  // block-uniform
   const int t = threadIdx.x;
   fill_rcp(s_rcp);  // visible after the first sub-tile's barriers
+  fill_nib_tab(s_nib);
   const int bucket = (int)work[3 * blockIdx.x + 0];
   const int64_t beg = work[3 * blockIdx.x + 1];
   const int64_t end = work[3 * blockIdx.x + 2];
@@ -680,9 +684,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))
   for (int i = t; i < kGenesPerBucket * kGeneCntPad; i += kBlock) s_cbin[i] = 0;
   for (int i = t; i < kGenesPerBucket * 3 * kStreamLanes; i += kBlock) s_lbin[i] = 0ull;
   if (*gwide)  // block-uniform
-    gene_reduce_item<false>(pay, beg, end, g0, s_buf, s_cbin, s_lbin, s_cnt, s_start, s_scan, s_rcp, s_uytab);
+    gene_reduce_item<false>(pay, beg, end, g0, s_buf, s_cbin, s_lbin, s_cnt, s_start, s_scan, s_rcp, s_uytab, s_nib);
   else
-    gene_reduce_item<true>(pay, beg, end, g0, s_buf, s_cbin, s_lbin, s_cnt, s_start, s_scan, s_rcp, s_uytab);
+    gene_reduce_item<true>(pay, beg, end, g0, s_buf, s_cbin, s_lbin, s_cnt, s_start, s_scan, s_rcp, s_uytab, s_nib);
   __syncthreads();
   // bins -> partial rows: counter lanes 0..14 are partial slots 0..14; stream lanes follow P_FLOAT
   for (int i = t; i < kGenesPerBucket * kGeneCnt; i += kBlock) {
