@@ -73,7 +73,7 @@ ALG_BYTES = {
 # HIP-event kernel names (engine profile) -> rocprofv3 kernel names (tools/pmc_traffic.py keys)
 # engine profile names -> the kernels (rocprofv3 names, sct::k_*) launched under them; a name
 # covering several kernels gets their dispatch-weighted mean bytes per launch
-PMC_NAMES = {"build_keys": ["build_keys_run"], "heads": ["heads4", "heads"],
+PMC_NAMES = {"build_keys": ["build_keys_run"], "heads": ["heads4", "heads"], "fill": ["fill_spans"],
              "scan": ["scan_wide", "scan_reduce", "scan_small", "scan_apply"],
              "tag_pack": ["pack"], "tag_keys": ["field_keys", "round_keys"], "tag_ties": ["tie_wave", "tie_wave2"],
              "tag_pack_keys": ["pack_field_keys"],
@@ -125,9 +125,13 @@ def parse():
                     help="config 5: the order sorted inside every step -- (CB, UB, GE) then query name, as "
                          "bam.sort_by_tags_and_queryname (bam.py:698-709) / TagSortBam define it (default), "
                          "or CB only (all the cell and grouped gene metrics need)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json"),
-                    help="rocprofv3 --pmc per-kernel HBM bytes (tools/pmc_passes.sh) for roofline.traffic")
-    return ap.parse_args()
+    ap.add_argument("--traffic-json", default=None,
+                    help="rocprofv3 --pmc per-kernel HBM bytes (tools/pmc_passes.sh) for roofline.traffic "
+                         "(default: the committed round-5 file of this config, profiles/r05/pmc_traffic_c<N>.json)")
+    a = ap.parse_args()
+    if a.traffic_json is None:
+        a.traffic_json = os.path.join(ROOT, "profiles", "r05", "pmc_traffic_c%d.json" % a.config)
+    return a
 
 
 def log(*a):
