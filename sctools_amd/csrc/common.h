@@ -85,7 +85,10 @@ struct __attribute__((aligned(16))) GenePayload {
 };
 static_assert(sizeof(GenePayload) == 16, "gene payload must be 16 bytes");
 
-constexpr int kGenesPerBucket = 64;  // LDS bins of one gene bucket
+#ifndef SCT_GENES_PER_BUCKET
+#define SCT_GENES_PER_BUCKET 64
+#endif
+constexpr int kGenesPerBucket = SCT_GENES_PER_BUCKET;  // LDS bins of one gene bucket
 constexpr int kMaxGeneBuckets = 4096;  // n_gene_ids <= 262144 (gene-bucket arrays in dynamic LDS, <= 64 KB a block)
 
 }  // namespace sct
