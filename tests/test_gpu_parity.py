@@ -142,6 +142,33 @@ def test_gpu_generated_against_oracle(eng, seed, n, cells, genes, sigma):
     compare(gi[live], gf[live], oi[live], of[live], exact_floats=False)
 
 
+@pytest.mark.parametrize("layout", ["boundaries", "head_65", "one_giant"])
+def test_welford_head_entities(eng, layout):
+    """The Welford drop-in's entity classes against the oracle, bit for bit (finalize.h): lanes of
+    one entity (< 48 records), the head kernel (k_welford_head2: the 64 largest entities, 16 per
+    block, 16-record chunks, a 224-record LDS ring) and the other chains (k_welford_chains).  Entity
+    lengths sit on the class boundary (47 / 48 / 49), on and beside chunk and ring multiples, one
+    past a full head group (65 big entities), and a 300k-record entity beside short ones."""
+    from sctools_amd import engine as E
+
+    if layout == "boundaries":
+        sizes = [47, 48, 49, 1, 2, 15, 16, 17, 223, 224, 225, 239, 240, 241, 4096, 4097, 5000]
+    elif layout == "head_65":
+        sizes = [3000 + 37 * i for i in range(65)] + [48] * 5 + [30] * 20
+    else:
+        sizes = [300_000, 60, 49, 48, 47, 3] + [700] * 10
+    n = int(sum(sizes))
+    d = gpu_synth(n, 50, 3_000, 91 + len(sizes))
+    cell = np.repeat(np.arange(len(sizes), dtype=np.int32), np.asarray(sizes))
+    d.cols["cell"] = torch.from_numpy(cell).to(eng.device)
+    h = host_cols(d)
+    dims = E.Dims(max(d.n_cell_ids, len(sizes)), d.n_gene_ids, d.n_umi_ids)
+    mito = torch.from_numpy(d.gene_is_mito).to(eng.device)
+    oi, of = O.run(h, "cell", d.gene_is_mito, d.n_gene_ids, threads=8)
+    gi, gf = eng.compute(d.cols, "cell", dims, mito, mito, float_mode="welford")
+    compare(gi.cpu().numpy(), gf.cpu().numpy(), oi, of, exact_floats=True)
+
+
 def test_properties_at_scale(eng):
     """Size-independent invariants on 20M records (the oracle would take too long)."""
     from sctools_amd import engine as E
