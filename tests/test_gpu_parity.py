@@ -169,6 +169,27 @@ def test_welford_head_entities(eng, layout):
     compare(gi.cpu().numpy(), gf.cpu().numpy(), oi, of, exact_floats=True)
 
 
+def test_welford_head_entities_gene_mode(eng):
+    """The same kernels in the gene view's three-stream form (GatherGeneMetrics' entities are
+    genes): gene runs of boundary lengths, 70 big genes and one 200k-record gene."""
+    from sctools_amd import engine as E
+
+    sizes = [200_000, 47, 48, 49, 224, 225] + [2000 + 29 * i for i in range(70)] + [5] * 30
+    n = int(sum(sizes))
+    d = gpu_synth(n, 300, 3_000, 97)
+    gene = np.repeat(np.arange(len(sizes), dtype=np.int32), np.asarray(sizes))
+    d.cols["gene"] = torch.from_numpy(gene).to(eng.device)
+    h = host_cols(d)
+    n_genes = max(d.n_gene_ids, len(sizes))
+    mito_np = np.zeros(n_genes, dtype=np.uint8)
+    mito_np[: d.gene_is_mito.shape[0]] = d.gene_is_mito
+    dims = E.Dims(d.n_cell_ids, n_genes, d.n_umi_ids)
+    mito = torch.from_numpy(mito_np).to(eng.device)
+    oi, of = O.run(h, "gene", mito_np, n_genes, threads=8)
+    gi, gf = eng.compute(d.cols, "gene", dims, mito, mito, float_mode="welford")
+    compare(gi.cpu().numpy(), gf.cpu().numpy(), oi, of, exact_floats=True)
+
+
 def test_properties_at_scale(eng):
     """Size-independent invariants on 20M records (the oracle would take too long)."""
     from sctools_amd import engine as E
