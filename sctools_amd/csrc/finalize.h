@@ -486,11 +486,10 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
   }
 }
 
-// Round 5: the head entities' chains on four waves of one block (k_welford_head2), kW2Ents entities
-// per block.  Inside the pipeline the lone wave of k_welford_chains carrying the longest entity ran
-// 1.7x (config 2) its pace alone: while the concurrent kernels keep HBM busy a load takes many
-// microseconds, and one 32-record batch of prefetch (~1 us of its chain) left it waiting (2.6x
-// beside an HBM copy, 2.4x beside FP64 work on its SIMD, tools/debug/welford_head2_micro.hip).  Here
+// Round 5: the head entities' chains on one block of 16 waves each (k_welford_head2), kW2Ents
+// entities per block.  Inside the pipeline the lone wave of k_welford_chains carrying the longest
+// entity ran at 1.7x (config 2) its pace alone; beside an HBM copy on every CU a chain runs at 2.6x,
+// beside FP64 work on its SIMD at 2.4x (tools/debug/welford_head2_micro.hip).  Here
 //   wave 0 (mean)   runs the mean chain alone on plain FP64 operations: per chunk of kW2Chunk records
 //                   it reads the chunk's samples and reciprocal pairs from LDS into registers, steps
 //                   the means (delta = x - mean, t = RN(l delta), q = RN(h delta + t), mean += q: the
@@ -500,14 +499,17 @@ __global__ void __launch_bounds__(kBlock) k_welford_chains(const int64_t* __rest
 //                   m2 += delta * d2 (stats.py:82-87: the same roundings in the same order) from the
 //                   staged samples and means; a lane's final mean is taken here at its last record
 //                   (chunks a lane finishes take a slower path with selects; finished lanes sit out);
-//   waves 2, 3      the loaders, kW2Depth chunks (~1000 records, ~27 us of the chain) ahead, copy the
-//   (loaders)       samples HBM -> LDS with direct-to-LDS loads (16 B per lane, 32 / kW2Ents records of
-//                   the block's entities per load, no registers in flight; each loader holds <= 60
-//                   loads in flight, below vmcnt's 63) and compute the chunk's reciprocal pairs;
-//                   loader w takes the chunks j with j % 2 == w.
-// Few entities per block keep the bytes per chain step small, so the LDS ring reaches far ahead.  The
-// waves meet at one block barrier per chunk (LDS writes done first; the loader of the chunk the next
-// phase reads waits for it).
+//   waves 2, 3      the loaders, kW2Depth chunks ahead (224 records at 16 entities per block: ~6 us
+//   (loaders)       of the chain), copy the samples HBM -> LDS with direct-to-LDS loads (16 B per
+//                   lane, 32 / kW2Ents records of the block's entities per load, no registers in
+//                   flight; each loader holds <= 63 loads in flight, vmcnt's limit) and compute the
+//                   chunk's reciprocal pairs; loader w takes the chunks j with j % 2 == w;
+//   waves 4 - 15    hold the CU's registers (below).
+// The waves meet at one block barrier per chunk (LDS writes done first; the loader of the chunk the
+// next phase reads waits for it).  16 entities per block measured best (4 / 8 per block have deeper
+// rings but more blocks: profiles/r05/welford/head_ents_per_block_c2.txt); the ~148 KB of LDS and
+// the register-holding waves give every head block a CU of its own, and welford_stage starts the
+// key pass only once the head blocks are resident (k_wf_gate).
 #ifndef SCT_W2_CHUNK
 #define SCT_W2_CHUNK 16
 #endif
@@ -531,7 +533,7 @@ static_assert(kW2Chunk % kW2PerLoad == 0 && kWfHeadEnts % kW2Ents == 0, "whole l
 static_assert((kW2Slots & (kW2Slots - 1)) == 0 && kW2Slots >= kW2Depth + 2, "slots: chunks p - 1 .. p + depth");
 constexpr int kW2InFlight = (kW2Depth / 2) * kW2Loads;  // a loader's loads in flight after issuing
 constexpr int kW2After = (kW2Depth / 2 - 1) * kW2Loads;  // ... after its chunk the next phase reads
-static_assert(kW2InFlight <= 63, "a loader's loads in flight fit vmcnt");
+static_assert(kW2InFlight <= 63, "a loader's loads in flight fit vmcnt");  // (56 at 16 entities)
 // The block barrier of k_welford_head2: LDS writes done, then s_barrier -- without the fence of
 // __syncthreads(), which also waits for every load in flight.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
