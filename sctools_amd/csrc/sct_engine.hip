@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <vector>
 
 #include "comm.h"
 #include "common.h"
@@ -370,10 +371,50 @@ int launch_build_keys(bool cell, bool gene, dim3 grid, hipStream_t s, const KeyC
 // only the mean / variance slots of the output rows (k_finalize writes the others), so it runs on a
 // side stream from the moment the entity starts exist, beside the key pass' successors (bucket
 // partition, hash tiles) on the caller's stream.
-// The two side streams are created once per device and process (round 4: creating them per call
-// cost ~0.6 ms of host time before the first Welford launch); concurrent pipelines on one device
-// share them (their kernels then queue behind each other; every call waits on its own events).
+// The side streams come from a per-device pool of (s2, s3) pairs created once and reused (round 4:
+// creating them per call cost ~0.6 ms of host time before the first Welford launch).  A call holds
+// its pair until it returns, so concurrent pipelines on one device get pairs of their own (round 5:
+// a shared pair queued one pipeline's head kernel behind another's, and the start gate then held
+// the second pipeline's key pass for its whole time-out).
+constexpr int kMaxSideDevices = 64;
+struct SidePool {
+  std::mutex mu;
+  std::vector<std::pair<hipStream_t, hipStream_t>> free[kMaxSideDevices];
+};
+SidePool& side_pool() {
+  static SidePool p;
+  return p;
+}
+hipError_t side_streams(int dev, hipStream_t* s2, hipStream_t* s3) {  // (the caller has set `dev` current)
+  if (dev < 0 || dev >= kMaxSideDevices) return hipErrorInvalidDevice;
+  SidePool& p = side_pool();
+  {
+    std::lock_guard<std::mutex> g(p.mu);
+    if (!p.free[dev].empty()) {
+      *s2 = p.free[dev].back().first;
+      *s3 = p.free[dev].back().second;
+      p.free[dev].pop_back();
+      return hipSuccess;
+    }
+  }
+  hipStream_t a = nullptr, b = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&a, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&b, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    if (a) (void)hipStreamDestroy(a);
+    return e;
+  }
+  *s2 = a;
+  *s3 = b;
+  return hipSuccess;
+}
+void side_streams_release(int dev, hipStream_t s2, hipStream_t s3) {
+  SidePool& p = side_pool();
+  std::lock_guard<std::mutex> g(p.mu);
+  p.free[dev].emplace_back(s2, s3);
+}
 struct WelfordSide {
+  int dev = -1;
   hipStream_t s2 = nullptr, s3 = nullptr;
   hipEvent_t fork = nullptr, join = nullptr, fork3 = nullptr, join3 = nullptr;
   ~WelfordSide() {  // the caller's stream waits on `join` and `join3` before anything after the pipeline
@@ -381,26 +422,9 @@ struct WelfordSide {
     if (join) (void)hipEventDestroy(join);
     if (fork3) (void)hipEventDestroy(fork3);
     if (join3) (void)hipEventDestroy(join3);
+    if (s2) side_streams_release(dev, s2, s3);  // (work still queued on them stays in order)
   }
 };
-constexpr int kMaxSideDevices = 64;
-hipError_t side_streams(int dev, hipStream_t* s2, hipStream_t* s3) {
-  static std::mutex mu;
-  static hipStream_t ss[kMaxSideDevices][2] = {};
-  if (dev < 0 || dev >= kMaxSideDevices) return hipErrorInvalidDevice;
-  std::lock_guard<std::mutex> g(mu);
-  for (int i = 0; i < 2; i++)
-    if (!ss[dev][i]) {
-      const hipError_t e = hipStreamCreateWithFlags(&ss[dev][i], hipStreamNonBlocking);
-      if (e != hipSuccess) {
-        ss[dev][i] = nullptr;
-        return e;
-      }
-    }
-  *s2 = ss[dev][0];
-  *s3 = ss[dev][1];
-  return hipSuccess;
-}
 
 int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent, const RecCols& rc2,
                   const int64_t* ent_start, double* out_f, hipStream_t s, WelfordSide& wf) {
@@ -411,6 +435,7 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
   HIPCHK(hipGetDevice(&prev));
   if (prev != dev) HIPCHK(hipSetDevice(dev));
   hipError_t ce = side_streams(dev, &wf.s2, &wf.s3);
+  if (ce == hipSuccess) wf.dev = dev;
   if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.fork, hipEventDisableTiming);
   if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.join, hipEventDisableTiming);
   if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.fork3, hipEventDisableTiming);
