@@ -109,7 +109,7 @@ __device__ __forceinline__ int64_t ent_end(const int64_t* __restrict__ ent_start
   return (e + 1 < n_ent) ? ent_start[e + 1] : n;
 }
 
-// big entities counted per log2 size class (wave-aggregated)
+// big entities counted per log2 size class
 // (round 5: counted per block in LDS first -- one global atomic per (block, size class) instead of
 // one per entity on 32 addresses: 0.2 ms each at config 4)
 __global__ void __launch_bounds__(kBlock) k_welford_bins(const int64_t* __restrict__ ent_start, int64_t n_ent,
@@ -713,6 +713,8 @@ __global__ void __launch_bounds__(kW2Waves * kWave) k_welford_head2(const int64_
 constexpr int64_t kWfGateTicks = 400000;  // 4 ms
 __global__ void __launch_bounds__(kWave) k_wf_gate(const uint32_t* started, uint32_t want, int64_t max_ticks) {
   const int64_t t0 = wall_clock64();
+  // (the index term is always 0: it keeps the poll a per-lane vector load, which sees the head
+  // blocks' global atomics, where a scalar-cache load of a uniform address might not)
   while (__hip_atomic_load(started + (threadIdx.x & kWave), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want &&
          wall_clock64() - t0 < max_ticks)
     __builtin_amdgcn_s_sleep(4);
