@@ -6,17 +6,24 @@ resident in HBM: per-cell metrics (RUN mode over the cell-sorted records) plus
 per-gene metrics (grouped per-gene partials, an RCCL all-reduce across ranks
 when N > 1, finalize), with both sets of entity rows copied back to the host.
 
-Workload: per rank 100M cell-sorted records over
-10k cells (lognormal(0,1) reads per cell), 30k genes (Zipf 1.1, plus None and
-multi-gene ids), 10-mer UMIs; generated on the GPU.  Ranks hold disjoint
-cells (the SplitBam cell-sharding invariant), so N GPUs process N x 100M
-records: weak scaling.
+Workload: 100M cell-sorted records over 10k cells
+(lognormal(0,1) reads per cell), 30k genes (Zipf 1.1, plus None and multi-gene
+ids), 10-mer UMIs; generated on the GPU.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+* N = 1: config 2 (the default).
+* N > 1: config 3 by default (BASELINE.json: "Same 100M-read workload ... across
+  2/4/8 GPUs"): every rank generates the SAME 100M-record set and keeps its
+  SplitBam-style shard -- a contiguous cell range balanced by record count
+  (distributed.shard_bounds) -- so N GPUs split one 100M-record job: strong
+  scaling, value = 100M x steps / max-over-ranks time.  `--config 2` at N > 1
+  gives each rank its own 100M records of disjoint cells instead (weak scaling).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
        (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 Rank 0 prints ONE JSON line.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -117,10 +124,12 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-check", action="store_true",
                     help="skip the record-count sanity checks (timing experimental engine builds only)")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5],
-                    help="2: cell-sorted records (default); 4: the 1B-read atlas per GPU of 8 -- 125M records, 62.5k "
-                         "cells with lognormal(0, 2) reads; 5: globally shuffled records, 30%% NH>1, 40%% duplicates, "
-                         "sorted by cell on the GPU inside every step (SURVEY.md 8(d) configs 4, 5)")
+    ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
+                    help="2: cell-sorted records per rank (default at N = 1; weak scaling at N > 1); 3: ONE 100M-record "
+                         "config-2 set split over the N ranks by cell ranges (default at N > 1; strong scaling); 4: the "
+                         "1B-read atlas per GPU of 8 -- 125M records, 62.5k cells with lognormal(0, 2) reads; 5: globally "
+                         "shuffled records, 30%% NH>1, 40%% duplicates, sorted by cell on the GPU inside every step "
+                         "(SURVEY.md 8(d) configs 3, 4, 5)")
     ap.add_argument("--sort-order", default="cell_umi_gene", choices=["cell_umi_gene", "cell"],
                     help="config 5: the order sorted inside every step -- (CB, UB, GE) then query name, as "
                          "bam.sort_by_tags_and_queryname (bam.py:698-709) / TagSortBam define it (default), "
@@ -129,8 +138,10 @@ def parse():
                     help="rocprofv3 --pmc per-kernel HBM bytes (tools/pmc_passes.sh) for roofline.traffic "
                          "(default: the committed round-5 file of this config, profiles/r05/pmc_traffic_c<N>.json)")
     a = ap.parse_args()
-    if a.traffic_json is None:
-        a.traffic_json = os.path.join(ROOT, "profiles", "r05", "pmc_traffic_c%d.json" % a.config)
+    if a.config is None:
+        a.config = 2 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 3
+    if a.traffic_json is None:  # (config 3 at N = 1 is config 2)
+        a.traffic_json = os.path.join(ROOT, "profiles", "r06", "pmc_traffic_c%d.json" % (2 if a.config == 3 else a.config))
     return a
 
 
@@ -167,14 +178,21 @@ def main():
     t0 = time.time()
     if args.config == 4:
         args.records, args.cells = 125_000_000, 62_500
+    strong = args.config == 3  # one record set split over the ranks (every rank generates it, keeps its shard)
     cfg = synth.SynthConfig(n_reads=args.records, n_cells=args.cells, n_genes=args.genes,
-                            sigma=2.0 if args.config == 4 else 1.0, seed=args.seed + 1000 * rank,
+                            sigma=2.0 if args.config == 4 else 1.0, seed=args.seed + (0 if strong else 1000 * rank),
                             umi_bits=args.umi_bits)
     if args.config == 5:  # 30 % NH > 1, 40 % duplicates, secondary alignments sharing a query name
         cfg.p_nh1, cfg.p_dup, cfg.p_secondary = 0.70, 0.40, 0.10
     data = synth.generate(cfg, device=dev, chunk=16_000_000)
     qname, n_qnames = None, 0
     n_cell_ids = data.n_cell_ids
+    shard_lo, shard_hi = 0, args.records
+    if strong and world > 1:  # SplitBam's cell-range shard of the one set (bam.py:361-488)
+        shard_lo, shard_hi = D.shard_bounds(data.cols["cell"], world)[rank]
+        data.cols = {c: t[shard_lo:shard_hi].clone() for c, t in data.cols.items()}
+        torch.cuda.empty_cache()
+    my_records = shard_hi - shard_lo
     if args.config == 5:  # global permutation: the step must regroup records itself
         g = torch.Generator(device=dev)
         g.manual_seed(args.seed + 1 + 1000 * rank)
@@ -279,11 +297,16 @@ def main():
         t = torch.tensor([n_cell_reads], dtype=torch.int64, device=dev)
         dist.all_reduce(t)
         n_cell_reads = int(t.item()) // world
+    if strong and world > 1:  # the shards' cell rows together cover the one set
+        t = torch.tensor([n_cell_reads], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        n_cell_reads = int(t.item())
+    job_records = args.records if strong else args.records * world
     if not args.no_check:
-        assert n_cell_reads == args.records, (n_cell_reads, args.records)
-        assert int(host_genei[:, 0].sum()) == args.records * world
+        assert n_cell_reads == (my_records if not strong else args.records), (n_cell_reads, args.records)
+        assert int(host_genei[:, 0].sum()) == job_records
 
-    total_records = args.records * world * args.steps
+    total_records = job_records * args.steps
     value = total_records / elapsed
     # dominant kernel: largest total in the profiling pass; its average launch time comes from the HIP
     # events that bracketed only its launches in the timed region (on its launch stream)
@@ -291,7 +314,7 @@ def main():
     # reports them per launch; the records of the shard where a launch does not report them)
     dom_ms, dom_launches, dom_items = prof.get(dom_name, (0.0, 1, -1))
     avg_s = dom_ms / 1e3 / max(1, dom_launches)
-    items_per_launch = dom_items / max(1, dom_launches) if dom_items >= 0 else float(args.records)
+    items_per_launch = dom_items / max(1, dom_launches) if dom_items >= 0 else float(my_records)
     per_launch_bytes = ALG_BYTES.get(dom_name, 0) * items_per_launch
     achieved = per_launch_bytes / avg_s if avg_s > 0 else 0.0
     roofline = {
@@ -308,11 +331,12 @@ def main():
         "alg_bytes_per_item": ALG_BYTES.get(dom_name, 0),
         "items_per_launch": items_per_launch,
         "items_source": "engine (per launch)" if dom_items >= 0 else "records of the shard",
-        # SURVEY.md 8(d)'s model of a sort pipeline (B_alg = 32 + 12 + 24*P + 44 bytes/record, a
-        # 7-pass LSD sort this pipeline does not run): a yardstick, not this pipeline's traffic
-        "model_alg_bytes_per_record": pipeline_bytes(args, dims),
-        "model_frac": value / world * pipeline_bytes(args, dims) / PEAK_HBM,
     }
+    # SURVEY.md 8(d)'s model of a sort pipeline (B_alg = 32 + 12 + 24*P + 44 bytes/record: a 7-pass LSD
+    # sort that this pipeline does NOT run) -- a yardstick kept outside `roofline`, not a measured fraction
+    sort_model = {"note": "SURVEY.md 8(d) 7-pass LSD sort model; not this pipeline's traffic, not measured",
+                  "model_256B_alg_bytes_per_record": pipeline_bytes(args, dims),
+                  "model_256B_frac": value / world * pipeline_bytes(args, dims) / PEAK_HBM}
     traffic = pmc_traffic(args, dom_name)
     if traffic is not None:
         roofline["traffic"], roofline["traffic_source"] = traffic
@@ -338,20 +362,23 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (SURVEY.md 8(d) config-%d generator, generated on GPU)" % args.config,
             "config": {
                 "workload": ({2: "config2: %d cell-sorted records/rank",
+                              3: "config3: ONE set of %d cell-sorted records split over the ranks by cell ranges "
+                                 "balanced by records (SplitBam's invariant)",
                               4: "config4: %d cell-sorted records/rank, lognormal(0, 2) reads per cell",
                               5: "config5: %d globally shuffled records/rank (30%% NH>1, 40%% dup, secondary alignments), "
                                  + ("records of every rank's cells dealt to every rank, cell bins swapped over RCCL "
                                     "each step, then " if world > 1 else "")
                                  + "GPU sort by " + ("(CB, UB, GE, query name)" if args.sort_order != "cell" else "CB")}
-                             [args.config]) % args.records + ", %d cells/rank, %d genes; cell metrics + grouped gene metrics%s"
-                            % (args.cells, args.genes, " + RCCL all-reduce" if world > 1 else ""),
-                "records_per_rank": args.records,
+                             [args.config]) % args.records + ", %d cells%s, %d genes; cell metrics + grouped gene metrics%s"
+                            % (args.cells, "" if strong else "/rank", args.genes, " + RCCL all-reduce" if world > 1 else ""),
+                "records_per_rank": my_records if strong else args.records,
+                "records_per_job": job_records,
                 "cells_per_rank": args.cells,
                 "genes": args.genes,
                 "float_mode": args.float_mode,
@@ -359,6 +386,7 @@ def main():
                 "parallelism": "cell-sharded x%d" % world + (" (rehearsal: ranks share cuda:0, gloo)" if share else ""),
             },
             "roofline": roofline,
+            "sort_model_yardstick": sort_model,
             "kernel_ms_per_step": kernel_ms_per_step,
             "kernel_items_per_step": kernel_items_per_step,
             "kernel_table_source": "untimed profiling pass of %d steps (HIP events around every kernel)" % PROFILE_STEPS,
@@ -366,11 +394,14 @@ def main():
             "speedup_vs_cpu_baseline": (value / cpu["value"]) if cpu else None,
             "reference_python": REFERENCE_PYTHON,
             "allreduce_ms": allreduce_ms,
+            # the job's gene rows (all ranks' partials summed): equal for config 2 at N = 1 and config 3
+            # at any N (exact-sum lanes), a check of the strong-scaling split
+            "gene_rows_sha256": hashlib.sha256(host_genei.numpy().tobytes() + host_genef.numpy().tobytes()).hexdigest(),
         }
         out.update(side)
         if "h2d" in side:
             per_step_s = elapsed / args.steps + (side["h2d"]["ms"] + side["count_entities_ms"]) / 1e3
-            out["records_per_s_incl_h2d_and_count"] = args.records * world / per_step_s
+            out["records_per_s_incl_h2d_and_count"] = job_records / per_step_s
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -479,7 +510,8 @@ def _traffic_file(args):
     w = d.get("workload", "")
     cfg = int(w.split("--config ")[1].split()[0].rstrip(":")) if "--config " in w else 2
     sizes = {2: (100_000_000, 10_000), 4: (125_000_000, 62_500), 5: (100_000_000, 10_000)}[cfg]
-    if cfg != args.config or (args.records, args.cells) != sizes:
+    ours = 2 if args.config == 3 and int(os.environ.get("WORLD_SIZE", "1")) == 1 else args.config
+    if cfg != ours or (args.records, args.cells) != sizes:
         return None
     return d
 

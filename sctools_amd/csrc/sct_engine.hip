@@ -380,20 +380,25 @@ constexpr int kMaxSideDevices = 64;
 struct SidePool {
   std::mutex mu;
   std::vector<std::pair<hipStream_t, hipStream_t>> free[kMaxSideDevices];
+  int in_use[kMaxSideDevices] = {};  // pairs held by running calls, per device
 };
 SidePool& side_pool() {
   static SidePool p;
   return p;
 }
-hipError_t side_streams(int dev, hipStream_t* s2, hipStream_t* s3) {  // (the caller has set `dev` current)
+// *alone: no other call on this device holds a pair (so no other pipeline's Welford kernels can
+// share a hardware queue with this one's)
+hipError_t side_streams(int dev, hipStream_t* s2, hipStream_t* s3, bool* alone) {  // (`dev` is current)
   if (dev < 0 || dev >= kMaxSideDevices) return hipErrorInvalidDevice;
   SidePool& p = side_pool();
   {
     std::lock_guard<std::mutex> g(p.mu);
+    *alone = p.in_use[dev] == 0;
     if (!p.free[dev].empty()) {
       *s2 = p.free[dev].back().first;
       *s3 = p.free[dev].back().second;
       p.free[dev].pop_back();
+      p.in_use[dev]++;
       return hipSuccess;
     }
   }
@@ -406,12 +411,15 @@ hipError_t side_streams(int dev, hipStream_t* s2, hipStream_t* s3) {  // (the ca
   }
   *s2 = a;
   *s3 = b;
+  std::lock_guard<std::mutex> g(p.mu);
+  p.in_use[dev]++;
   return hipSuccess;
 }
 void side_streams_release(int dev, hipStream_t s2, hipStream_t s3) {
   SidePool& p = side_pool();
   std::lock_guard<std::mutex> g(p.mu);
   p.free[dev].emplace_back(s2, s3);
+  p.in_use[dev]--;
 }
 struct WelfordSide {
   int dev = -1;
@@ -434,7 +442,8 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
   HIPCHK(hipStreamGetDevice(s, &dev));
   HIPCHK(hipGetDevice(&prev));
   if (prev != dev) HIPCHK(hipSetDevice(dev));
-  hipError_t ce = side_streams(dev, &wf.s2, &wf.s3);
+  bool alone = true;
+  hipError_t ce = side_streams(dev, &wf.s2, &wf.s3, &alone);
   if (ce == hipSuccess) wf.dev = dev;
   if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.fork, hipEventDisableTiming);
   if (ce == hipSuccess) ce = hipEventCreateWithFlags(&wf.join, hipEventDisableTiming);
@@ -465,25 +474,37 @@ int welford_stage(const Layout& L, void* ws, bool cell, int64_t n, int64_t n_ent
     // (config 2).  The key pass (the caller's stream) and the sample pass (s3) first wait on the
     // device, boundedly, for the head blocks to be resident (k_wf_gate).  A scheduling aid only: on
     // the time-out they go on, and nothing waits on them.
+    // Round 6: the head kernels are submitted before the gates, so a gate that lands on
+    // the head stream's hardware queue (4 per process) sits behind them instead of holding them up
+    // for its whole time-out; and the gates are left out when another call on this device holds a
+    // side-stream pair (concurrent pipelines: their head blocks compete for the same CUs, so one
+    // pipeline's gate could wait on CUs another pipeline holds).
     const uint32_t* started = &wch->started;
     constexpr unsigned kHeadBlocks = (unsigned)(kWfHeadEnts / kW2Ents);
-    HIPCHK(hipStreamWaitEvent(s, wf.fork3, 0));
-    LAUNCH("welford_gate", k_wf_gate, dim3(1), dim3(kWave), s, started, kHeadBlocks, kWfGateTicks);
-    LAUNCH("welford_gate", k_wf_gate, dim3(1), dim3(kWave), s3, started, kHeadBlocks, kWfGateTicks);
+    const char* nogate = getenv("SCT_NO_WF_GATE");
+    const bool gate = alone && !(nogate && nogate[0] == '1');
     if (cell) {
       LAUNCH("welford_x_head", k_welford_x_ents<true>, hgrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n,
              (const uint32_t*)worder, (const WelfordCtl*)wch, xs);
       LAUNCH_N("welford_head", n, k_welford_head2<true>, dim3(kHeadBlocks), dim3(kW2Waves * kWave), s2, ent_start,
                n_ent, n, (const uint32_t*)worder, wch, (const double*)xs, out_f);
-      LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s3, rc2, n, xs, ent_start, n_ent,
-               (const uint32_t*)worder, (const uint32_t*)&wch->n_big);
-      LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,
-               (const uint32_t*)worder, wc, (const double*)xs, out_f);
     } else {
       LAUNCH("welford_x_head", k_welford_x_ents<false>, hgrid, dim3(kBlock), s2, rc2, ent_start, n_ent, n,
              (const uint32_t*)worder, (const WelfordCtl*)wch, xs);
       LAUNCH_N("welford_head", n, k_welford_head2<false>, dim3(kHeadBlocks), dim3(kW2Waves * kWave), s2, ent_start,
                n_ent, n, (const uint32_t*)worder, wch, (const double*)xs, out_f);
+    }
+    if (gate) {
+      HIPCHK(hipStreamWaitEvent(s, wf.fork3, 0));
+      LAUNCH("welford_gate", k_wf_gate, dim3(1), dim3(kWave), s, started, kHeadBlocks, kWfGateTicks);
+      LAUNCH("welford_gate", k_wf_gate, dim3(1), dim3(kWave), s3, started, kHeadBlocks, kWfGateTicks);
+    }
+    if (cell) {
+      LAUNCH_N("welford_x", n, k_welford_x<true>, xgrid, dim3(kBlock), s3, rc2, n, xs, ent_start, n_ent,
+               (const uint32_t*)worder, (const uint32_t*)&wch->n_big);
+      LAUNCH_N("welford_chains", n, k_welford_chains<true>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,
+               (const uint32_t*)worder, wc, (const double*)xs, out_f);
+    } else {
       LAUNCH_N("welford_x", n, k_welford_x<false>, xgrid, dim3(kBlock), s3, rc2, n, xs, ent_start, n_ent,
                (const uint32_t*)worder, (const uint32_t*)&wch->n_big);
       LAUNCH_N("welford_chains", n, k_welford_chains<false>, dim3(kWfBlocks), dim3(kBlock), s3, ent_start, n_ent, n,

@@ -162,7 +162,7 @@ struct ProfScope {
 // Several small fills in one launch (round 5: the step issued ~10 hipMemsetAsync calls, each its
 // own ~5 us kernel).  Span k gets the byte value val[k] (memset semantics); blockIdx.y picks the span,
 // 16-byte stores where the span allows them.
-constexpr int kFillSpans = 10;
+constexpr int kFillSpans = 12;
 struct FillSpans {
   uint8_t* p[kFillSpans];
   uint64_t bytes[kFillSpans];
@@ -188,8 +188,13 @@ __global__ void __launch_bounds__(256) k_fill_spans(FillSpans f) {
 struct FillBatch {
   FillSpans f{};
   uint64_t most = 0;
+  bool overflow = false;  // a span past kFillSpans: launch_fills fails instead of dropping it
   void add(void* p, size_t bytes, uint8_t val = 0) {
     if (!bytes) return;
+    if (f.n >= kFillSpans) {
+      overflow = true;
+      return;
+    }
     f.p[f.n] = static_cast<uint8_t*>(p);
     f.bytes[f.n] = bytes;
     f.val[f.n] = val;
@@ -498,6 +503,7 @@ __device__ __forceinline__ void wave_flush_packed16(int32_t (&v)[K], bool member
 
 namespace sct {
 inline int launch_fills(FillBatch& fb, hipStream_t s) {
+  if (fb.overflow) return fail(SCT_EINVAL, "internal: more than %d fill spans in one batch", kFillSpans);
   if (!fb.f.n) return SCT_OK;
   uint64_t blocks = (fb.most / 16 + 255) / 256;
   blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);

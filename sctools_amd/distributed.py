@@ -49,6 +49,22 @@ def shard_bounds(entity, world: int) -> List[Tuple[int, int]]:
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
+def balanced_cell_bins(cell_counts, world: int) -> np.ndarray:
+    """Cell id -> bin (uint8) for the cell-bin exchange: contiguous cell-id (barcode) ranges balanced
+    by record count, so bin order is barcode order and a few large cells cannot land together in
+    one bin of an equal-id-range split.  A cell goes to the bin that holds the midpoint of its
+    records in the cumulative count (non-decreasing in the cell id)."""
+    if not 1 <= world <= 256:
+        raise ValueError("world must be in [1, 256]")
+    c = np.asarray(cell_counts, dtype=np.int64)
+    total = int(c.sum())
+    if total == 0 or world == 1:
+        return np.zeros(max(1, c.shape[0]), np.uint8)
+    mid2 = 2 * (np.cumsum(c) - c) + c  # twice the midpoint of each cell's records
+    b = (mid2 * world) // (2 * total)
+    return np.minimum(b, world - 1).astype(np.uint8)
+
+
 def shard(cols, lo: int, hi: int):
     """The record range [lo, hi) of every column (contiguous views)."""
     return {k: v[lo:hi] for k, v in cols.items()}
@@ -63,13 +79,48 @@ def allreduce_partials(partials: torch.Tensor, group=None) -> torch.Tensor:
     return partials
 
 
+def pack_rows(cols: dict, tiebreak: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, list]:
+    """Records as one row-major int32 buffer [n, W / 4]: every column's bytes side by side (the 32-byte
+    record of SURVEY.md 8(d), + 4 bytes of tiebreak), so a bin moves in ONE collective.  Returns the
+    buffer and the layout (name, dtype, byte offset, bytes) for unpack_rows."""
+    names = list(cols) + (["_tie"] if tiebreak is not None else [])
+    ts = [cols[c] for c in cols] + ([tiebreak] if tiebreak is not None else [])
+    n = int(ts[0].numel()) if ts else 0
+    layout, parts, off = [], [], 0
+    for name, t in zip(names, ts):
+        w = t.element_size()
+        parts.append(t.contiguous().view(torch.uint8).view(n, w))
+        layout.append((name, t.dtype, off, w))
+        off += w
+    pad = (-off) % 4
+    if pad:
+        parts.append(torch.zeros((n, pad), dtype=torch.uint8, device=ts[0].device))
+    rows = torch.cat(parts, dim=1) if parts else torch.zeros((0, 4), dtype=torch.uint8)
+    return rows.view(torch.int32), layout
+
+
+def unpack_rows(rows: torch.Tensor, layout) -> Tuple[dict, Optional[torch.Tensor]]:
+    """pack_rows' inverse: (columns, tiebreak or None), each a fresh contiguous tensor."""
+    n = int(rows.shape[0])
+    b = rows.contiguous().view(torch.uint8).view(n, -1)
+    cols, tie = {}, None
+    for name, dt, off, w in layout:
+        t = b[:, off:off + w].contiguous().view(dt).view(n)
+        if name == "_tie":
+            tie = t
+        else:
+            cols[name] = t
+    return cols, tie
+
+
 def exchange_records(binned: dict, tiebreak: Optional[torch.Tensor], counts: torch.Tensor,
                      group=None) -> Tuple[dict, Optional[torch.Tensor], List[int]]:
     """The cell-bin swap between ranks (SplitBam's bins, bam.py:439-480, as a collective): bin p of
     this rank's ``binned`` columns (``counts[p]`` records, bins consecutive in bin order, as
     ``Engine.bin_records`` lays them out) goes to rank p; this rank receives rank 0's bin for it,
-    then rank 1's, ... -- file order when rank r holds the r-th part of the file.  One
-    all_to_all of the counts, then one per column (RCCL with the ``nccl`` backend, gloo on CPU).
+    then rank 1's, ... -- file order when rank r holds the r-th part of the file.  One all_to_all of
+    the counts, then ONE of the records packed as rows (pack_rows: the 32-byte record + the 4-byte
+    tiebreak; RCCL with the ``nccl`` backend, gloo on CPU).
     Returns (columns, tiebreak or None, received counts per source rank)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if counts.numel() != world:
@@ -88,23 +139,12 @@ def exchange_records(binned: dict, tiebreak: Optional[torch.Tensor], counts: tor
     dist.all_to_all_single(recv, send, group=group)
     send_l, recv_l = send.tolist(), recv.tolist()
     total = int(sum(recv_l))
-
-    def swap(t):
-        src = io(t.contiguous())
-        dt = src.dtype
-        # 8- and 16-bit columns: gloo has no such all_to_all types (widened to int32 and back); RCCL
-        # moves 16-bit words as float16 (a plain copy, bits unchanged)
-        if dist.get_backend(group) == "gloo" and dt in (torch.int16, torch.uint8, torch.int8):
-            src = src.to(torch.int32)
-        elif dt == torch.int16:
-            src = src.view(torch.float16)
-        out = torch.empty((total,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
-        dist.all_to_all_single(out, src, output_split_sizes=recv_l, input_split_sizes=send_l, group=group)
-        out = out.to(dt) if out.dtype == torch.int32 and dt != torch.int32 else out.view(dt)
-        return out.to(dev) if host else out
-
-    cols = {c: swap(t) for c, t in binned.items()}
-    tie = swap(tiebreak) if tiebreak is not None else None
+    rows, layout = pack_rows(binned, tiebreak)
+    src = io(rows)
+    out = torch.empty((total, src.shape[1]), dtype=src.dtype, device=src.device)
+    dist.all_to_all_single(out, src, output_split_sizes=recv_l, input_split_sizes=send_l, group=group)
+    del rows, src
+    cols, tie = unpack_rows(out.to(dev) if host else out, layout)
     return cols, tie, [int(x) for x in recv_l]
 
 

@@ -20,18 +20,23 @@ attribute from the engine's row.  ``finalize`` of an aggregator that parsed
 nothing gives the reference's values (zero counts, 0.0 means, NaN variances
 and ratios) without a launch.
 
-A record that raises part-way (round 5): the reference has by then fed it to some
-of its state.  A mapped read without an XF or NH tag (``KeyError``, aggregator.py:305 / 317) has
-reached its molecule and fragment histograms and its UY / genomic Welford streams (264-303), so it
-is buffered with the fields read so far before the error propagates; ``finalize()`` then takes the
-distinct counts and the streams from the engine (that record included) and keeps the host's
-integer counters, which stopped exactly where the reference's stopped.  A caller that catches the
-error and calls ``finalize()`` -- at once, or after parsing more records -- gets the reference's
-values (tests/golden/protocol: ``final_after_error``, ``final_continued``).  Remaining gap: a
-record that raises earlier -- ``KeyError`` on CR (after its CY sample, 507-520) or UY, or
-``TypeError`` / ``ZeroDivisionError`` on its qualities (after its UY sample) -- has fed only part of
-a record's streams, which the engine's record format cannot express; it is not buffered, so
-``finalize()`` after catching such an error leaves it out of the streams and distinct counts.
+A record that raises part-way (rounds 5-6): the reference has by then fed
+it to some of its state, in its own order (aggregator.py:257-334, 507-530):
+
+* CR missing under a CB (cell, 518): its CY sample only (507-514);
+* UY missing or empty (270): the subclass fields (CY sample, the gene / cell histogram), n_reads and
+  the molecule histogram (259-264);
+* no or empty base qualities (288): those and the UY sample (266-273);
+* a mapped read without XF or NH (305 / 317): all of it up to and including the fragment
+  histogram (303) and both genomic streams (287-292).
+
+Each buffered record carries the set of the reference's states it fed ("fed" bits).  ``finalize()``
+takes the distinct counts and ratios from an engine run over the records that reached n_reads (a
+record that stopped before its fragment histogram marked unmapped there, so it adds a molecule but
+no fragment), and each Welford stream from an engine run over exactly the records that fed that
+stream, in file order; the host's integer counters stopped exactly where the reference's stopped.
+A caller that catches the error and calls ``finalize()`` -- at once, or after parsing more records
+-- gets the reference's values (tests/golden/protocol: ``final_after_error``, ``final_continued``).
 """
 
 from typing import Sequence
@@ -81,7 +86,7 @@ class MetricAggregator:
         self.fragments_per_molecule: float = None
         self.fragments_with_single_read_evidence: int = None
         self.molecules_with_single_read_evidence: int = None
-        self._buffered = []  # (tags, numeric fields) per parsed record
+        self._buffered = []  # (tags, numeric fields, fed bits) per parsed record
         self._extra = (0, 0)  # the subclass's CY counts of the record being parsed
 
     # ---- aggregator protocol (aggregator.py:236-340) ----
@@ -89,47 +94,46 @@ class MetricAggregator:
         """aggregator.py:251-334, record by record: the subclass fields first, then the counters,
         raising where the reference raises.
 
-        A mapped read without an XF or NH tag is buffered before its KeyError propagates (the
-        reference has counted it in its histograms and streams by then; see the module docstring)."""
+        A record that raises part-way is buffered with the states the reference fed before the
+        exception propagates (see the module docstring)."""
         for record in records:
-            self._extra = (0, 0)
-            self.parse_extra_fields(tags=tags, record=record)
-            cg, cl = self._extra
+            self._extra = None
+            try:
+                self.parse_extra_fields(tags=tags, record=record)
+            except Exception:
+                if self._extra is not None:  # cell: the CY sample was taken, CR raised (518)
+                    self._buffer(tags, record, FED_CY, cy=self._extra)
+                raise
+            cy = self._extra if self._extra is not None else (0, 0)
+            fed = FED_CORE | FED_CY
             self.n_reads += 1
-            ug, ul = C._frac_counts(record.get_tag(consts.QUALITY_MOLECULE_BARCODE_TAG_KEY))
+            try:
+                uy = C._frac_counts(record.get_tag(consts.QUALITY_MOLECULE_BARCODE_TAG_KEY))
+            except (KeyError, ZeroDivisionError):  # after the molecule histogram (264-270)
+                self._buffer(tags, record, fed, cy=cy)
+                raise
+            fed |= FED_UY
             try:
                 self.perfect_molecule_barcodes += record.get_tag(
                     consts.RAW_MOLECULE_BARCODE_TAG_KEY) == record.get_tag(consts.MOLECULE_BARCODE_TAG_KEY)
             except KeyError:
                 pass
             aq = record.query_alignment_qualities
-            if aq is None:
-                raise TypeError("'NoneType' object is not iterable")
-            if len(aq) == 0:
+            if aq is None or len(aq) == 0:  # _quality_above_threshold (288): after the UY sample
+                self._buffer(tags, record, fed, cy=cy, uy=uy)
+                if aq is None:
+                    raise TypeError("'NoneType' object is not iterable")
                 raise ZeroDivisionError("division by zero")
+            fed |= FED_GQ
             flag = record.flag
-            b = C.B_PERFECT_UMI if _perfect_umi(record) else 0
-            cb = record.get_tag(consts.CELL_BARCODE_TAG_KEY) if record.has_tag(consts.CELL_BARCODE_TAG_KEY) else None
-            if cb is not None:
-                b |= C.B_HAS_CB
-                if self._MODE == "cell" and record.get_tag(consts.RAW_CELL_BARCODE_TAG_KEY) == cb:
-                    b |= C.B_PERFECT_CB
-            xfv = record.get_tag(consts.ALIGNMENT_LOCATION_TAG_KEY) if record.has_tag(
-                consts.ALIGNMENT_LOCATION_TAG_KEY) else None
-            x = C.XF_ABSENT if xfv is None else C._XF_CODE.get(xfv, C.XF_OTHER)
-            if flag & 0x10:
-                b |= C.B_REVERSE
-            if flag & 0x400:
-                b |= C.B_DUPLICATE
             s = sum(aq)
             gq = (s, len(aq), sum(1 for q in aq if q > 30))
-            if flag & 0x4:
-                b |= C.B_UNMAPPED
-            else:
+            if not flag & 0x4:
+                fed |= FED_FRAG  # the fragment histogram (303) precedes the XF / NH reads
                 try:
                     alignment_location = record.get_tag(consts.ALIGNMENT_LOCATION_TAG_KEY)
                 except KeyError:
-                    self._buffer_partial(tags, record, gq, b, x, cg, cl, ug, ul)
+                    self._buffer(tags, record, fed, cy=cy, uy=uy, gq=gq)
                     raise
                 if alignment_location == consts.CODING_ALIGNMENT_LOCATION_TAG_VALUE:
                     self.reads_mapped_exonic += 1
@@ -140,11 +144,10 @@ class MetricAggregator:
                 try:
                     nh = record.get_tag(consts.NUMBER_OF_HITS_TAG_KEY)
                 except KeyError:
-                    self._buffer_partial(tags, record, gq, b, x, cg, cl, ug, ul)
+                    self._buffer(tags, record, fed, cy=cy, uy=uy, gq=gq)
                     raise
                 if nh == 1:
                     self.reads_mapped_uniquely += 1
-                    b |= C.B_NH1
                 else:
                     self.reads_mapped_multiple += 1
                 if flag & 0x400:
@@ -153,21 +156,52 @@ class MetricAggregator:
                     record.get_cigar_stats()[0][3]
                 if n_len:
                     self.spliced_reads += 1
-                    b |= C.B_SPLICED
                 self._plus_strand_reads += not (flag & 0x10)
-            if not _fits(gq, cl, ul):
+            else:
+                nh = n_len = None
+            num = self._fields(record, cy, uy, gq, nh, n_len)
+            if num is None:
                 raise ValueError("record %s exceeds the 32-byte columnar limits" % getattr(record, "query_name", "?"))
-            num = (record.reference_id, record.pos) + gq + (b, x, cg, cl, ug, ul)
-            self._buffered.append((tuple(tags), num))
+            self._buffered.append((tuple(tags), num, FED_ALL))
 
-    def _buffer_partial(self, tags, record, gq, b, x, cg, cl, ug, ul) -> None:
-        """A mapped read about to raise KeyError on XF or NH (aggregator.py:305 / 317): buffered as
-        the reference has consumed it -- its molecule and fragment keys and its stream samples -- so
-        the engine's distinct counts and streams include it; the XF / NH counters it never reached are
-        the host's (_fill keeps them).  A record past the columnar limits stays out (the KeyError
-        still propagates)."""
-        if _fits(gq, cl, ul):
-            self._buffered.append((tuple(tags), (record.reference_id, record.pos) + gq + (b, x, cg, cl, ug, ul)))
+    def _fields(self, record, cy, uy, gq, nh=None, n_len=None):
+        """The record's 32-byte numeric fields (columnar.record_fields' layout); a stream the record
+        never reached gets a neutral stand-in sample (a = 0, b = 1: its run never reports that stream).
+        None if a field exceeds its column width."""
+        cy = cy if cy is not None else (0, 1)
+        uy = uy if uy is not None else (0, 1)
+        gq = gq if gq is not None else (0, 1, 0)
+        if not _fits(gq, cy[1], uy[1]):
+            return None
+        flag = record.flag
+        b = C.B_PERFECT_UMI if _perfect_umi(record) else 0
+        cb = record.get_tag(consts.CELL_BARCODE_TAG_KEY) if record.has_tag(consts.CELL_BARCODE_TAG_KEY) else None
+        if cb is not None:
+            b |= C.B_HAS_CB
+            if self._MODE == "cell" and record.has_tag(consts.RAW_CELL_BARCODE_TAG_KEY) and \
+                    record.get_tag(consts.RAW_CELL_BARCODE_TAG_KEY) == cb:
+                b |= C.B_PERFECT_CB
+        xfv = record.get_tag(consts.ALIGNMENT_LOCATION_TAG_KEY) if record.has_tag(
+            consts.ALIGNMENT_LOCATION_TAG_KEY) else None
+        x = C.XF_ABSENT if xfv is None else C._XF_CODE.get(xfv, C.XF_OTHER)
+        if flag & 0x10:
+            b |= C.B_REVERSE
+        if flag & 0x400:
+            b |= C.B_DUPLICATE
+        if flag & 0x4:
+            b |= C.B_UNMAPPED
+        if nh == 1:
+            b |= C.B_NH1
+        if n_len:
+            b |= C.B_SPLICED
+        return (record.reference_id, record.pos) + tuple(gq) + (b, x, cy[0], cy[1], uy[0], uy[1])
+
+    def _buffer(self, tags, record, fed, cy=None, uy=None, gq=None) -> None:
+        """A record about to raise, buffered with the states it fed (``fed`` bits).  A record past
+        the columnar limits stays out (the exception still propagates)."""
+        num = self._fields(record, cy, uy, gq)
+        if num is not None:
+            self._buffered.append((tuple(tags), num, fed))
 
     def parse_extra_fields(self, tags: Sequence[str], record) -> None:
         """Per-record hook of the subclasses (aggregator.py:336-340)."""
@@ -176,11 +210,35 @@ class MetricAggregator:
     def _run_engine(self, mitochondrial_genes=frozenset(), float_mode="welford"):
         from sctools_amd.metrics.single import aggregate_buffered
 
-        if not self._buffered:
+        buf = self._buffered
+        core = [i for i, (_, _, f) in enumerate(buf) if f & FED_CORE]
+
+        def run(idx, core_run):
+            items = []
+            for i in idx:
+                tags, num, f = buf[i]
+                if core_run and not f & FED_FRAG and not num[5] & C.B_UNMAPPED:
+                    # stopped before its fragment histogram (303): a molecule, but no fragment
+                    num = num[:5] + (num[5] | C.B_UNMAPPED,) + num[6:]
+                items.append((tags, num))
+            return aggregate_buffered(self._MODE, items, mitochondrial_genes, float_mode)
+
+        if core:
+            self._fill(*run(core, True))
+        else:
             self._fill_empty()
-            return
-        ints, floats = aggregate_buffered(self._MODE, self._buffered, mitochondrial_genes, float_mode)
-        self._fill(ints, floats)
+        # every Welford stream over exactly the records that fed it (file order)
+        for bit, names in _STREAMS[self._MODE]:
+            idx = [i for i, (_, _, f) in enumerate(buf) if f & bit]
+            if idx == core and core:
+                continue
+            if not idx:
+                vals = {n: (0.0 if n.endswith("_mean") else _NAN) for n in names}
+            else:
+                _, floats = run(idx, False)
+                vals = {n: float(floats[slot]) for n, kind, slot in R.columns_for(self._MODE) if n in names}
+            for n in names:
+                setattr(self, n, vals[n])
 
     def _fill_empty(self) -> None:
         """finalize() with nothing parsed (aggregator.py:350-387): Welford means 0.0 and variances NaN
@@ -206,6 +264,30 @@ class MetricAggregator:
     def finalize(self) -> None:
         self._run_engine()
 
+
+# the reference states a buffered record may have fed before raising (parse_molecule)
+FED_CORE = 1   # n_reads, the molecule histogram, the subclass histogram (aggregator.py:259-264, 530, 595)
+FED_UY = 2     # the UY Welford sample (266-273)
+FED_GQ = 4     # both genomic Welford samples (287-292)
+FED_CY = 8     # the CY Welford sample (cell, 507-514)
+FED_FRAG = 16  # the fragment histogram (303)
+FED_ALL = 31
+
+# the Welford streams of each mode: (fed bit, mean / variance attribute names)
+_STREAMS = {
+    "cell": ((FED_UY, ("molecule_barcode_fraction_bases_above_30_mean",
+                       "molecule_barcode_fraction_bases_above_30_variance")),
+             (FED_GQ, ("genomic_reads_fraction_bases_quality_above_30_mean",
+                       "genomic_reads_fraction_bases_quality_above_30_variance",
+                       "genomic_read_quality_mean", "genomic_read_quality_variance")),
+             (FED_CY, ("cell_barcode_fraction_bases_above_30_variance",
+                       "cell_barcode_fraction_bases_above_30_mean"))),
+    "gene": ((FED_UY, ("molecule_barcode_fraction_bases_above_30_mean",
+                       "molecule_barcode_fraction_bases_above_30_variance")),
+             (FED_GQ, ("genomic_reads_fraction_bases_quality_above_30_mean",
+                       "genomic_reads_fraction_bases_quality_above_30_variance",
+                       "genomic_read_quality_mean", "genomic_read_quality_variance"))),
+}
 
 # counters parse_molecule / parse_extra_fields keep record by record (aggregator.py:259-334, 507-527)
 _HOST_COUNTERS = frozenset((

@@ -291,6 +291,7 @@ class DeviceGroup:
         tie = torch.cat(ties) if tiebreak is not None else None
         torch.cuda.current_stream(dev).synchronize()
         g.before_collective(rank)  # every rank has its pieces
+        self._xslots[rank] = None  # (its binned copy is freed once the caller drops it)
         return out, tie
 
     def abort(self) -> None:
@@ -360,6 +361,21 @@ def _cells_twice(cols) -> bool:
         return int(torch.bincount(heads.long()).max().item()) > 1
     heads = cell[np.concatenate(([0], np.flatnonzero(cell[1:] != cell[:-1]) + 1))]
     return np.bincount(heads).max() > 1
+
+
+def cell_record_counts(cols, n_cell_ids: int) -> np.ndarray:
+    """Records per cell id over the whole record set (host or device columns, or decoded shards)."""
+    if isinstance(cols, columnar.ShardedColumns):
+        tot = np.zeros(max(1, n_cell_ids), np.int64)
+        for sh in cols.shards:
+            c = sh["cell"]
+            if c.shape[0]:
+                tot += torch.bincount(c.long(), minlength=tot.shape[0]).cpu().numpy()[: tot.shape[0]]
+        return tot
+    cell = cols.arrays["cell"]
+    if isinstance(cell, torch.Tensor):
+        return torch.bincount(cell.long(), minlength=max(1, n_cell_ids)).cpu().numpy().astype(np.int64)
+    return np.bincount(np.asarray(cell), minlength=max(1, n_cell_ids)).astype(np.int64)
 
 
 def cells_twice(cols) -> bool:
@@ -494,6 +510,8 @@ def sorted_cell_and_gene_rows(cols, mitochondrial_gene_ids=frozenset(), float_mo
         bounds = _bounds(cols, "cell", g.size)
         if g.size > N.SCT_MAX_BINS:
             raise ValueError("at most %d devices" % N.SCT_MAX_BINS)
+        # bins = contiguous barcode ranges balanced by record count (rank order stays barcode order)
+        table = D.balanced_cell_bins(cell_record_counts(cols, dims.n_cell_ids), g.size)
         g.comms()
 
         def rank_rows(r):
@@ -501,7 +519,8 @@ def sorted_cell_and_gene_rows(cols, mitochondrial_gene_ids=frozenset(), float_mo
             eng = g.engines[r]
             part = _rank_cols(cols, r, lo, hi, eng.device)
             tie = torch.from_numpy(tiebreak[lo:hi]).to(eng.device) if tiebreak is not None else None
-            binned, btie, counts = eng.bin_records(part, dims, g.size, tie)
+            bin_of_cell = torch.from_numpy(table).to(eng.device)
+            binned, btie, counts = eng.bin_records(part, dims, g.size, tie, bin_of_cell=bin_of_cell)
             del part, tie
             mine, mtie = g.exchange(r, binned, btie, counts)
             del binned, btie

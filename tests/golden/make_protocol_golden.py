@@ -9,7 +9,7 @@ Run here only (the reference never leaves this container):
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_protocol_golden.py
 
 Each case names an entity of a bundled BAM (its records in file order) and, optionally, one
-record to damage (a tag dropped, or no base qualities).  Recorded: the integer attributes after
+record to damage (a tag dropped, no base qualities, or empty aligned qualities).  Recorded: the integer attributes after
 each record, the exception type a record raised (the case stops there), and, for cases without
 an error, every public attribute after ``finalize()`` as ``str`` (the CSV text, writer.py:96).  An empty aggregator's
 ``finalize()`` is recorded too.  For a case whose damaged record raised, two more states (round 5):
@@ -66,6 +66,15 @@ CASES = [
     ("gene", "small-gene-sorted", 3, 20, "drop:NH"),
     ("gene", "small-gene-sorted", 7, 9, "drop:XF"),
     ("gene", "small-gene-sorted", 3, 2, "noqual"),
+    # round 6: more partial states -- the first record raising (nothing but a CY sample, or only the
+    # molecule histogram, fed), empty aligned qualities (all soft-clipped: ZeroDivisionError at 288)
+    ("cell", "small-cell-sorted", 22, 0, "drop:CR"),
+    ("cell", "small-cell-sorted", 14, 0, "drop:UY"),
+    ("cell", "small-cell-sorted", 17, 5, "emptyqual"),
+    ("cell", "small-cell-sorted", 14, 0, "noqual"),
+    ("cell", "cell-sorted-missing-cb", 28, 2, "drop:UY"),
+    ("gene", "small-gene-sorted", 4, 10, "emptyqual"),
+    ("gene", "small-gene-sorted", 3, 0, "drop:UY"),
 ]
 
 
@@ -91,6 +100,9 @@ def damaged(rec, damage):
         return seg
     if damage == "noqual":
         seg._aq = None
+        return seg
+    if damage == "emptyqual":  # every base soft-clipped: query_alignment_qualities is empty
+        seg._aq = seg._aq[:0]
         return seg
     tags = dict(seg._tags)
     tags.pop(damage.split(":")[1], None)

@@ -222,9 +222,11 @@ def test_aggregator_protocol_golden_finalize():
     assert done >= 8
 
 
-# damaged records whose partial state the aggregator reproduces: CY missing (nothing consumed yet)
-# and a mapped read without XF / NH (buffered as far as the reference consumed it)
-EXACT_AFTER_ERROR = ("drop:CY", "drop:XF", "drop:NH")
+# damaged records whose partial state the aggregator reproduces -- all of them since round 6: CY
+# missing (nothing consumed yet), CR missing (its CY sample only), UY missing (the molecule
+# histogram), no / empty aligned qualities (and the UY sample), a mapped read without XF / NH (up to
+# its fragment and genomic streams)
+EXACT_AFTER_ERROR = ("drop:CY", "drop:CR", "drop:UY", "noqual", "emptyqual", "drop:XF", "drop:NH")
 
 
 def _same_final(got, want, label):
@@ -263,7 +265,7 @@ def test_finalize_after_a_caught_error_matches_reference():
         agg.finalize()
         _same_final({k: v for k, v in vars(agg).items() if not k.startswith("_")}, case["final_continued"], label)
         done += 1
-    assert done >= 5
+    assert done >= 17
 
 
 @pytest.mark.parametrize("bam", H.BAMS)

@@ -58,7 +58,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, balanced=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -67,16 +67,33 @@ def _worker(rank, world, port, q):
         n = cols["cell"].shape[0]
         lo, hi = n * rank // world, n * (rank + 1) // world
         part = {c: a[lo:hi] for c, a in cols.items()}
-        b = bin_of(part["cell"], world, d.n_cell_ids)
+        if balanced:  # record-balanced barcode ranges (multigpu.sorted_cell_and_gene_rows' table)
+            table = D.balanced_cell_bins(np.bincount(cols["cell"], minlength=d.n_cell_ids), world)
+            bin_of_w = (lambda c, nb, nc: table[c].astype(np.int64))  # noqa: E731
+        else:
+            bin_of_w = bin_of
+        b = bin_of_w(part["cell"], world, d.n_cell_ids)
         order = np.argsort(b, kind="stable")
         binned = {c: torch.from_numpy(np.ascontiguousarray(a[order].view(np.int16) if a.dtype == np.uint16
                                                             else a[order])) for c, a in part.items()}
         tie = torch.from_numpy(np.ascontiguousarray(qname[lo:hi][order]))
         counts = torch.from_numpy(np.bincount(b, minlength=world).astype(np.int64))
-        got, gtie, recv = D.exchange_records(binned, tie, counts)
+        calls = []
+        a2a = dist.all_to_all_single
+
+        def counted(*a, **k):
+            calls.append(1)
+            return a2a(*a, **k)
+
+        dist.all_to_all_single = counted
+        try:
+            got, gtie, recv = D.exchange_records(binned, tie, counts)
+        finally:
+            dist.all_to_all_single = a2a
+        assert len(calls) == 2, "one collective for the counts, ONE for the packed records"
         mine = {c: (t.numpy().view(np.uint16) if t.dtype == torch.int16 else t.numpy()) for c, t in got.items()}
         # every record of this rank's cells, in global file order
-        want = bin_of(cols["cell"], world, d.n_cell_ids) == rank
+        want = bin_of_w(cols["cell"], world, d.n_cell_ids) == rank
         for c in cols:
             assert np.array_equal(mine[c], cols[c][want]), c
         assert np.array_equal(gtie.numpy(), qname[want])
@@ -89,12 +106,12 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_exchange_then_sort_equals_one_process(world):
+@pytest.mark.parametrize("world,balanced", [(2, False), (3, False), (3, True)])
+def test_exchange_then_sort_equals_one_process(world, balanced):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, balanced)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -126,3 +143,41 @@ def test_exchange_one_rank_is_identity():
     binned = {"cell": torch.arange(5, dtype=torch.int32)}
     got, tie, recv = D.exchange_records(binned, None, torch.tensor([5]))
     assert got["cell"] is binned["cell"] and tie is None and recv == [5]
+
+
+def test_pack_rows_round_trip():
+    """The exchange's packed rows: the 32-byte record (+ 4-byte tiebreak) per row, unpacked bit for bit."""
+    cols, qname, _ = shuffled_set(n=5000)
+    t = {c: torch.from_numpy(np.ascontiguousarray(a.view(np.int16) if a.dtype == np.uint16 else a))
+         for c, a in cols.items()}
+    tie = torch.from_numpy(np.ascontiguousarray(qname))
+    rows, layout = D.pack_rows(t, tie)
+    assert rows.dtype == torch.int32 and tuple(rows.shape) == (5000, 9)
+    got, gtie = D.unpack_rows(rows, layout)
+    assert list(got) == list(t)
+    for c in t:
+        assert got[c].dtype == t[c].dtype and torch.equal(got[c], t[c]), c
+    assert torch.equal(gtie, tie)
+    rows, layout = D.pack_rows(t, None)
+    assert tuple(rows.shape) == (5000, 8)
+    got, gtie = D.unpack_rows(rows, layout)
+    assert gtie is None and all(torch.equal(got[c], t[c]) for c in t)
+
+
+def test_balanced_cell_bins():
+    """Record-balanced barcode ranges: non-decreasing in the cell id (rank order = barcode order), every
+    bin used when the counts allow, and far better balanced than equal id ranges on skewed cells."""
+    rng = np.random.default_rng(3)
+    counts = np.sort(rng.lognormal(0, 2.0, 5000)).astype(np.int64)[::-1].copy()  # big cells first
+    counts[0] = 0  # (the missing-CB id may be empty)
+    for world in (1, 2, 3, 8, 64):
+        b = D.balanced_cell_bins(counts, world)
+        assert b.dtype == np.uint8 and b.shape == counts.shape
+        assert np.all(np.diff(b.astype(int)) >= 0) and b.max() < world
+        load = np.bincount(b, weights=counts, minlength=world)
+        ideal = counts.sum() / world
+        assert load.max() <= ideal + counts.max(), (world, load.max(), ideal)
+        if world > 1:
+            naive = np.bincount((np.arange(counts.size) * world) // counts.size, weights=counts, minlength=world)
+            assert load.max() < naive.max()
+    assert D.balanced_cell_bins(np.zeros(4, np.int64), 4).tolist() == [0, 0, 0, 0]

@@ -48,11 +48,14 @@ def damaged(r: BamRecord, damage):
         return r
     tags = dict(r._tags)
     qual = r._qual
+    cigar = r.cigar
     if damage == "noqual":
         qual = None
+    elif damage == "emptyqual":  # every base soft-clipped: empty aligned qualities
+        cigar = [(4, r.l_seq)]
     else:
         tags.pop(damage.split(":")[1], None)
-    return BamRecord(r.query_name, r.flag, r.reference_id, r.pos, r.mapq, r.cigar, r.l_seq, qual, tags)
+    return BamRecord(r.query_name, r.flag, r.reference_id, r.pos, r.mapq, cigar, r.l_seq, qual, tags)
 
 
 CASES = _load()["cases"]
@@ -103,7 +106,7 @@ def test_empty_finalize(kind):
 
 def test_protocol_golden_covers_the_error_paths():
     raised = {c["raised"] for c in CASES}
-    assert {"KeyError", "TypeError", None} <= raised
+    assert {"KeyError", "TypeError", "ZeroDivisionError", None} <= raised
     assert any(c["kind"] == "gene" and c["raised"] for c in CASES)
 
 
