@@ -27,7 +27,10 @@ constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
 static_assert(kRadix == kBlock, "digit-per-thread scan assumes kRadix == kBlock");
 
-__global__ void k_radix_upsweep(const uint64_t* __restrict__ keys, int64_t n, int shift, int64_t num_tiles,
+// K: uint64_t, or uint32_t for keys of <= 32 bits (round 6: the group tag sort's K1 -- a third less
+// traffic per pass)
+template <typename K = uint64_t>
+__global__ void k_radix_upsweep(const K* __restrict__ keys, int64_t n, int shift, int64_t num_tiles,
                                 uint32_t* __restrict__ counts) {
   __shared__ uint32_t hist[kWaves][kRadix];
   const int wid = threadIdx.x / kWave;
@@ -49,12 +52,13 @@ __global__ void k_radix_upsweep(const uint64_t* __restrict__ keys, int64_t n, in
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __restrict__ keys_in,
+template <typename K = uint64_t>
+__global__ void __launch_bounds__(kBlock) k_radix_downsweep(const K* __restrict__ keys_in,
                                                             const uint32_t* __restrict__ vals_in,
-                                                            uint64_t* __restrict__ keys_out,
+                                                            K* __restrict__ keys_out,
                                                             uint32_t* __restrict__ vals_out, int64_t n, int shift,
                                                             int64_t num_tiles, const uint32_t* __restrict__ offsets) {
-  __shared__ uint64_t s_keys[kSortTile];
+  __shared__ K s_keys[kSortTile];
   __shared__ uint32_t s_vals[kSortTile];
   __shared__ uint32_t s_whist[kWaves][kRadix];
   __shared__ uint32_t s_dstart[kRadix];
@@ -74,7 +78,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __re
   __syncthreads();
 
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  uint64_t k[kSortItems];
+  K k[kSortItems];
   uint32_t v[kSortItems];
   uint16_t rank[kSortItems];
   uint8_t dig[kSortItems];
@@ -87,7 +91,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __re
       k[j] = keys_in[p];
       v[j] = vals_in[p];
     } else {
-      k[j] = ~0ull;  // padding: digit 255 at every shift, ranked after all real items, never written
+      k[j] = (K)~0ull;  // padding: digit 255 at every shift, ranked after all real items, never written
       v[j] = 0;
     }
     const uint32_t d = (uint32_t)(k[j] >> shift) & (kRadix - 1);
@@ -133,7 +137,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const uint64_t* __re
   }
   __syncthreads();
   for (int q = threadIdx.x; q < tile_n; q += kBlock) {
-    const uint64_t kk = s_keys[q];
+    const K kk = s_keys[q];
     const uint32_t d = (uint32_t)(kk >> shift) & (kRadix - 1);
     const uint64_t o = (uint64_t)s_goff[d] + (uint32_t)(q - (int)s_dstart[d]);
     keys_out[o] = kk;
@@ -367,11 +371,41 @@ inline int radix_sort(const SortBuffers& B, int64_t n, int bits, int* which, hip
     const uint32_t* vin = cur ? B.vb : B.va;
     uint64_t* kout = cur ? B.ka : B.kb;
     uint32_t* vout = cur ? B.va : B.vb;
-    LAUNCH_N("radix_upsweep", n, k_radix_upsweep, dim3((unsigned)tiles), dim3(kBlock), s, kin, n, shift, tiles, B.counts);
+    LAUNCH_N("radix_upsweep", n, k_radix_upsweep<uint64_t>, dim3((unsigned)tiles), dim3(kBlock), s, kin, n, shift,
+             tiles, B.counts);
     int rc = scan_counts(B.counts, (int64_t)kRadix * tiles, B.offsets, B.sums, s);
     if (rc) return rc;
-    LAUNCH_N("radix_downsweep", n, k_radix_downsweep, dim3((unsigned)tiles), dim3(kBlock), s, kin, vin, kout, vout, n,
-           shift, tiles, (const uint32_t*)B.offsets);
+    LAUNCH_N("radix_downsweep", n, k_radix_downsweep<uint64_t>, dim3((unsigned)tiles), dim3(kBlock), s, kin, vin, kout,
+             vout, n, shift, tiles, (const uint32_t*)B.offsets);
+    cur ^= 1;
+  }
+  *which = cur;
+  return SCT_OK;
+}
+
+// the same over 32-bit keys (bits <= 32) held in the key buffers (ka / kb reinterpreted)
+inline int radix_sort32(const SortBuffers& B, int64_t n, int bits, int* which, hipStream_t s) {
+  if (bits > 32) return fail(SCT_EINVAL, "radix_sort32: %d key bits", bits);
+  const int passes = (bits + kRadixBits - 1) / kRadixBits;
+  const int64_t tiles = cdiv(n, kSortTile);
+  if ((int64_t)kRadix * tiles > B.count_cap)
+    return fail(SCT_EINVAL, "radix_sort32: %lld digit counts exceed the workspace's %lld", (long long)(kRadix * tiles),
+                (long long)B.count_cap);
+  uint32_t* ka = reinterpret_cast<uint32_t*>(B.ka);
+  uint32_t* kb = reinterpret_cast<uint32_t*>(B.kb);
+  int cur = 0;
+  for (int ps = 0; ps < passes; ps++) {
+    const int shift = ps * kRadixBits;
+    const uint32_t* kin = cur ? kb : ka;
+    const uint32_t* vin = cur ? B.vb : B.va;
+    uint32_t* kout = cur ? ka : kb;
+    uint32_t* vout = cur ? B.va : B.vb;
+    LAUNCH_N("radix_upsweep", n, k_radix_upsweep<uint32_t>, dim3((unsigned)tiles), dim3(kBlock), s, kin, n, shift,
+             tiles, B.counts);
+    int rc = scan_counts(B.counts, (int64_t)kRadix * tiles, B.offsets, B.sums, s);
+    if (rc) return rc;
+    LAUNCH_N("radix_downsweep", n, k_radix_downsweep<uint32_t>, dim3((unsigned)tiles), dim3(kBlock), s, kin, vin, kout,
+             vout, n, shift, tiles, (const uint32_t*)B.offsets);
     cur ^= 1;
   }
   *which = cur;

@@ -801,7 +801,7 @@ SortLayout sort_layout(int64_t n) {
   L.lva = take(sizeof(uint32_t) * (size_t)n1);
   L.lvb = take(sizeof(uint32_t) * (size_t)n1);
   L.longs = take(sizeof(uint4) * (size_t)(n1 / (kTieShort + 1) + 1));
-  L.tctl = take(2 * sizeof(uint32_t));
+  L.tctl = take(4 * sizeof(uint32_t));
   L.total = off;
   return L;
 }
@@ -1040,6 +1040,41 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
                 at<uint32_t>(workspace, L.vb), at<uint32_t>(workspace, L.counts), at<uint32_t>(workspace, L.offsets),
                 at<uint64_t>(workspace, L.sums), L.count_cap};
   const dim3 grid((unsigned)cdiv(n, kBlock));
+  // (CB, UB, GE[, query name]) by groups (tagsort.h, round 6): an LSD sort of (cell, top umi bits) only,
+  // then every group sorted inside its own positions
+  const char* grp_env = getenv("SCT_TAG_GROUP_SORT");
+  if (order == SCT_ORDER_CELL_UMI_GENE && !(grp_env && grp_env[0] == '0')) {
+    GroupBits gb{};
+    gb.c = f[0].bits, gb.u = f[1].bits, gb.g = f[2].bits, gb.t = tiebreak ? f[3].bits : 0;
+    const int ub_min = gb.u + gb.g + gb.t - 52 > 0 ? gb.u + gb.g + gb.t - 52 : 0;  // W fits 52 bits
+    const int passes = (gb.c + ub_min + kRadixBits - 1) / kRadixBits;
+    if (ub_min <= gb.u && passes <= 4) {
+      gb.ub = kRadixBits * passes - gb.c < gb.u ? kRadixBits * passes - gb.c : gb.u;  // fill the last digit
+      gb.ul = gb.u - gb.ub;
+      uint4* longs = at<uint4>(workspace, L.longs);
+      uint32_t* tctl = at<uint32_t>(workspace, L.tctl);
+      HIPCHK(hipMemsetAsync(tctl, 0, 4 * sizeof(uint32_t), s));
+      LAUNCH_N("tag_group_keys", n, k_pack_group_keys, grid, dim3(kBlock), s, *in, n, gb, tiebreak, recs,
+               reinterpret_cast<uint32_t*>(B.ka), B.va, tctl);
+      int which = 0;
+      rc = radix_sort32(B, n, gb.c + gb.ub, &which, s);
+      if (rc) return rc;
+      const uint32_t* keys = reinterpret_cast<const uint32_t*>(which ? B.kb : B.ka);
+      const uint32_t* perm = which ? B.vb : B.va;
+      uint2* glong = reinterpret_cast<uint2*>(longs);
+      LAUNCH_N("tag_group_wave", n, k_group_wave, grid, dim3(kBlock), s, keys, perm, (const uint4*)recs, n, gb, *out,
+               glong, tctl);
+      uint32_t h[3] = {0, 0, 0};
+      if (int rb = readback(h, tctl, sizeof(h), s)) return rb;
+      if (!h[1] && !h[2]) {
+        if (h[0])
+          LAUNCH("tag_group_long", k_group_long, dim3(h[0]), dim3(kBlock), s, keys, perm, (const uint4*)recs, gb,
+                 (const uint2*)glong, *out);
+        return SCT_OK;
+      }
+      // a group past kGroupCap records or a cell id the key cannot hold: the general path below
+    }
+  }
   int field_bits = 0;
   for (int i = 0; i < nf - (tiebreak ? 1 : 0); i++) field_bits += f[i].bits;
   if (!(tiebreak && field_bits <= 64)) LAUNCH_N("tag_pack", n, k_pack, grid, dim3(kBlock), s, *in, recs);

@@ -536,5 +536,223 @@ __global__ void __launch_bounds__(kBlock) k_long_scatter(const uint32_t* __restr
   perm[pos_of[j]] = cv[j];
 }
 
+// ---- (CB, UB, GE[, query name]) by groups (round 6) ----
+// The order's key is 14 + 20 + 15 (+ 27 query-name) bits at config 5; sorting all of it by device-wide
+// LSD passes took 7 passes plus a random gather of every record's tiebreak and row.  Instead:
+//   k_pack_group_keys  one pass over the SoA columns: the 32-byte row (the tiebreak in the cell's word:
+//                      the cell comes back from the key) and the GROUP key K1 = (cell, top `ub` umi bits);
+//   radix_sort         LSD over K1 only (c + ub bits: 3 passes at config 5), stable;
+//   k_group_wave       one wave per 64 sorted positions: every group (run of equal K1: ~10 records at
+//                      config 5) that lies in the wave is sorted by W = (low umi bits, gene, tiebreak,
+//                      lane) with one 64-lane bitonic network -- the lane is the input order inside a
+//                      group (the LSD passes are stable), so ties keep it as sorted() does -- and the
+//                      group crossing the wave's end (<= 64 records) by a second network; each record's
+//                      row is gathered once and written to the SoA output in its final place;
+//   k_group_long       groups of 65 .. kGroupCap records: one block each, a bitonic sort in LDS.
+// A group longer than kGroupCap (or a cell id the key cannot hold) sets a flag, and the host sorts
+// with the general path instead.
+constexpr int kGroupCap = 2048;  // records of a long group sorted in one block's LDS (11 index bits)
+struct GroupBits {
+  int ub;   // umi bits in K1 (the top ones)
+  int ul;   // umi bits below them (in W)
+  int g, t; // gene and tiebreak bits (in W)
+  int c, u; // cell and umi bits
+};
+
+__device__ __forceinline__ uint32_t low_bits(uint32_t v, int b) { return b >= 32 ? v : (v & ((1u << b) - 1u)); }
+
+// W: the order inside a group, < 2^52 (the host picks ub so that ul + g + t <= 52)
+__device__ __forceinline__ uint64_t group_w(uint32_t tie, uint32_t umi, uint32_t gene, const GroupBits& gb) {
+  const uint64_t ul = (uint64_t)low_bits(umi, gb.ul);
+  const uint64_t gv = (uint64_t)low_bits(gene, gb.g);
+  const uint64_t tv = gb.t ? (uint64_t)low_bits(tie, gb.t) : 0ull;
+  return (ul << (gb.g + gb.t)) | (gv << gb.t) | tv;
+}
+
+// ctl[0]: long groups listed, ctl[1]: a group longer than kGroupCap, ctl[2]: a cell id >= 2^c
+__global__ void __launch_bounds__(kBlock) k_pack_group_keys(sct_records_t r, int64_t n, GroupBits gb,
+                                                            const int32_t* __restrict__ tie, uint4* __restrict__ rows,
+                                                            uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                            uint32_t* __restrict__ ctl) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t cell = (uint32_t)r.cell[j], umi = (uint32_t)r.umi[j];
+  if (low_bits(cell, gb.c) != cell) atomicOr(&ctl[2], 1u);
+  rows[2 * j] = make_uint4(tie ? (uint32_t)tie[j] : 0u, umi, (uint32_t)r.gene[j], (uint32_t)r.ref[j]);
+  rows[2 * j + 1] = make_uint4((uint32_t)r.pos[j], (uint32_t)r.gq_sum[j] | ((uint32_t)r.gq_len[j] << 16),
+                               (uint32_t)r.gq_gt30[j] | ((uint32_t)r.bits[j] << 16) | ((uint32_t)r.xf[j] << 24),
+                               (uint32_t)r.cy_gt30[j] | ((uint32_t)r.cy_len[j] << 8) | ((uint32_t)r.uy_gt30[j] << 16) |
+                                   ((uint32_t)r.uy_len[j] << 24));
+  const uint32_t top = gb.ub ? (low_bits(umi, gb.u) >> gb.ul) : 0u;
+  keys[j] = (uint32_t)(((uint64_t)low_bits(cell, gb.c) << gb.ub) | top);  // c + ub <= 32
+  vals[j] = (uint32_t)j;
+}
+
+// one record to the SoA output (its cell from the group key, the rest from its row)
+__device__ __forceinline__ void group_store(const sct_records_t& out, int64_t j, uint32_t cell, const uint4& a,
+                                            const uint4& b) {
+  const_cast<int32_t*>(out.cell)[j] = (int32_t)cell;
+  const_cast<int32_t*>(out.umi)[j] = (int32_t)a.y;
+  const_cast<int32_t*>(out.gene)[j] = (int32_t)a.z;
+  const_cast<int32_t*>(out.ref)[j] = (int32_t)a.w;
+  const_cast<int32_t*>(out.pos)[j] = (int32_t)b.x;
+  const_cast<uint16_t*>(out.gq_sum)[j] = (uint16_t)(b.y & 0xFFFFu);
+  const_cast<uint16_t*>(out.gq_len)[j] = (uint16_t)(b.y >> 16);
+  const_cast<uint16_t*>(out.gq_gt30)[j] = (uint16_t)(b.z & 0xFFFFu);
+  const_cast<uint8_t*>(out.bits)[j] = (uint8_t)(b.z >> 16);
+  const_cast<uint8_t*>(out.xf)[j] = (uint8_t)(b.z >> 24);
+  const_cast<uint8_t*>(out.cy_gt30)[j] = (uint8_t)b.w;
+  const_cast<uint8_t*>(out.cy_len)[j] = (uint8_t)(b.w >> 8);
+  const_cast<uint8_t*>(out.uy_gt30)[j] = (uint8_t)(b.w >> 16);
+  const_cast<uint8_t*>(out.uy_len)[j] = (uint8_t)(b.w >> 24);
+}
+
+// 64-lane bitonic sort of one 64-bit key per lane, ascending by lane
+__device__ __forceinline__ uint64_t bitonic64_key(uint64_t key, int lane) {
+#pragma unroll
+  for (int size = 2; size <= kWave; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint64_t ok = __shfl_xor(key, stride);
+      const bool asc = (lane & size) == 0 || size == kWave;
+      const bool low = (lane & stride) == 0;
+      key = (low == asc) ? (ok < key ? ok : key) : (ok > key ? ok : key);
+    }
+  }
+  return key;
+}
+
+// the row of lane `src`
+__device__ __forceinline__ void row_from(int src, uint4& a, uint4& b) {
+  a.y = (uint32_t)__shfl((int)a.y, src);
+  a.z = (uint32_t)__shfl((int)a.z, src);
+  a.w = (uint32_t)__shfl((int)a.w, src);
+  b.x = (uint32_t)__shfl((int)b.x, src);
+  b.y = (uint32_t)__shfl((int)b.y, src);
+  b.z = (uint32_t)__shfl((int)b.z, src);
+  b.w = (uint32_t)__shfl((int)b.w, src);
+}
+
+// The group crossing the wave's end is found from a halo of the next 64 keys, so its records' loads
+// are issued together with the wave's own (one round of dependent loads, not two).
+__global__ void __launch_bounds__(kBlock) k_group_wave(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ perm,
+                                                       const uint4* __restrict__ rows, int64_t n, GroupBits gb,
+                                                       sct_records_t out, uint2* __restrict__ longs,
+                                                       uint32_t* __restrict__ ctl) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t p0 = p - lane;
+  const bool valid = p < n;
+  const uint32_t k = valid ? keys[p] : 0u;
+  const int64_t ph = p + kWave;
+  const uint32_t hk = ph < n ? keys[ph] : 0u;  // the halo
+  uint32_t kp = (uint32_t)__shfl_up((int)k, 1), kn = (uint32_t)__shfl_down((int)k, 1);
+  if (lane == 0) kp = (p > 0 && valid) ? keys[p - 1] : ~k;
+  if (lane == kWave - 1) kn = (p + 1 < n) ? keys[p + 1] : ~k;
+  const bool head = !valid || k != kp;
+  const bool tail = !valid || p + 1 >= n || k != kn;
+  const uint64_t H = __ballot(head), T = __ballot(tail);
+  const uint64_t upto = lane == kWave - 1 ? ~0ull : ((2ull << lane) - 1);
+  const uint64_t from = ~((1ull << lane) - 1);
+  const uint64_t hs = H & upto, ts = T & from;
+  const int s0 = hs ? 63 - __clzll((long long)hs) : -1;  // first lane of the lane's group, if in this wave
+  const int s1 = ts ? __ffsll((unsigned long long)ts) - 1 : -1;  // last lane of the group, if in this wave
+  const bool inside = valid && s0 >= 0 && s1 >= 0;  // the lane's group lies in the wave: written here
+  // the group crossing the wave's end, if it starts in this wave (else an earlier wave owns it)
+  const bool cross = !((T >> (kWave - 1)) & 1ull) && H != 0;  // wave-uniform
+  const int h = cross ? 63 - __clzll((long long)H) : 0;
+  const uint32_t kl = (uint32_t)__shfl((int)k, kWave - 1);
+  const uint64_t same = __ballot(ph < n && hk == kl);
+  const int ext = same == ~0ull ? kWave : __builtin_ctzll(~same);
+  const int64_t g0 = p0 + h;
+  const int L = kWave - h + ext;
+  const bool small = cross && ext < kWave && L <= kWave;
+  uint32_t idx = 0, idx2 = 0;
+  if (inside) idx = perm[p];
+  const bool in2 = small && lane < L;
+  if (in2) idx2 = perm[g0 + lane];
+  uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0), a2 = a, b2 = a;
+  if (inside) {
+    a = rows[2 * (int64_t)idx];
+    b = rows[2 * (int64_t)idx + 1];
+  }
+  if (in2) {
+    a2 = rows[2 * (int64_t)idx2];
+    b2 = rows[2 * (int64_t)idx2 + 1];
+  }
+  const bool need = inside && s1 > s0;
+  if (__ballot(need)) {
+    // (group start lane | W | lane): lanes outside groups key on their own lane and stay put
+    const uint64_t w = need ? group_w(a.x, a.y, a.z, gb) : 0ull;
+    const uint64_t key = bitonic64_key(((uint64_t)(need ? s0 : lane) << 58) | (w << 6) | (uint64_t)lane, lane);
+    row_from((int)(key & 63u), a, b);
+  }
+  if (inside) group_store(out, p, k >> gb.ub, a, b);
+  if (!cross) return;  // wave-uniform
+  if (small) {
+    const uint64_t key = bitonic64_key(in2 ? ((group_w(a2.x, a2.y, a2.z, gb) << 6) | (uint64_t)lane) : ~0ull, lane);
+    row_from((int)(key & 63u), a2, b2);
+    if (in2) group_store(out, g0 + lane, kl >> gb.ub, a2, b2);
+    return;
+  }
+  // longer than a wave: its end, 64 keys at a time past the halo (bounded by kGroupCap)
+  int64_t e = ph - lane + ext;
+  if (ext == kWave) {
+    while (true) {
+      const int64_t q = e + lane;
+      const uint64_t m = __ballot(q < n && keys[q] == kl);
+      const int x = m == ~0ull ? kWave : __builtin_ctzll(~m);
+      e += x;
+      if (x < kWave || e - g0 > kGroupCap) break;
+    }
+  }
+  const int64_t len = e - g0;
+  if (len > kGroupCap) {
+    if (lane == 0) atomicOr(&ctl[1], 1u);  // too long: the host sorts on the general path
+  } else if (lane == 0) {
+    longs[atomicAdd(&ctl[0], 1u)] = make_uint2((uint32_t)g0, (uint32_t)len);
+  }
+}
+
+// one block per long group (65 .. kGroupCap records): (W, index) bitonic-sorted in LDS
+__global__ void __launch_bounds__(kBlock) k_group_long(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ perm,
+                                                       const uint4* __restrict__ rows, GroupBits gb,
+                                                       const uint2* __restrict__ longs, sct_records_t out) {
+  __shared__ uint64_t s_k[kGroupCap];
+  const uint2 G = longs[blockIdx.x];
+  const int len = (int)G.y;
+  int np2 = kWave;
+  while (np2 < len) np2 <<= 1;
+  for (int i = threadIdx.x; i < np2; i += kBlock) {
+    uint64_t v = ~0ull;
+    if (i < len) {
+      const uint4 a = rows[2 * (int64_t)perm[G.x + i]];
+      v = (group_w(a.x, a.y, a.z, gb) << 11) | (uint64_t)i;
+    }
+    s_k[i] = v;
+  }
+  __syncthreads();
+  for (int size = 2; size <= np2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < np2 / 2; i += kBlock) {
+        const int lo = 2 * i - (i & (stride - 1));  // pair (lo, lo + stride)
+        const int hi = lo + stride;
+        const bool asc = (lo & size) == 0;
+        const uint64_t x = s_k[lo], y = s_k[hi];
+        if ((x > y) == asc) {
+          s_k[lo] = y;
+          s_k[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const uint32_t cell = keys[G.x] >> gb.ub;
+  for (int j = threadIdx.x; j < len; j += kBlock) {
+    const uint32_t idx = perm[G.x + (uint32_t)(s_k[j] & (kGroupCap - 1))];
+    group_store(out, (int64_t)G.x + j, cell, rows[2 * (int64_t)idx], rows[2 * (int64_t)idx + 1]);
+  }
+}
+
 }  // namespace sct
 

@@ -175,6 +175,29 @@ def test_sorted_rows_over_devices_equal_one_device(eng, devices, float_mode, tie
     assert np.array_equal(np.nan_to_num(got_gene[1], nan=-1.0), np.nan_to_num(want_gene[1], nan=-1.0))
 
 
+@pytest.mark.parametrize("float_mode,tie", [("exact", False), ("welford", True)])
+def test_sorted_rows_over_two_gpus_equal_one_device(eng, float_mode, tie):
+    """the multi-device exchange over RCCL (sct_exchange_counts / sct_exchange_records with
+    two ranks on two GPUs: the per-peer send / recv groups, the non-shared-device path) against one
+    device sorting everything.  Skipped on a one-GPU box -- the case the round-end driver runs on an
+    8-GPU node."""
+    from sctools_amd import multigpu
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    d, cols, qname = _shuffled(2_000_000, seed=22)
+    want_cell, want_gene = _one_device_rows(eng, d, cols, qname, float_mode, tie)
+    got_cell, got_gene = multigpu.sorted_cell_and_gene_rows(
+        _as_columns(d, cols), float_mode=float_mode, devices=[0, 1], tiebreak=qname.cpu().numpy() if tie else None,
+        n_tiebreak_ids=d.extra["n_qnames"] if tie else 0)
+    ent = [i for i in range(N.SCT_NI) if i != N.I_ENTITY]
+    assert np.array_equal(got_cell[0][:, ent], want_cell[0][:, ent])
+    assert np.array_equal(np.nan_to_num(got_cell[1], nan=-1.0), np.nan_to_num(want_cell[1], nan=-1.0))
+    assert np.array_equal(got_cell[2], want_cell[2])
+    assert np.array_equal(got_gene[0], want_gene[0])
+    assert np.array_equal(np.nan_to_num(got_gene[1], nan=-1.0), np.nan_to_num(want_gene[1], nan=-1.0))
+
+
 @pytest.mark.parametrize("devices", [1, [0, 0, 0]])
 def test_unsorted_bam_cell_and_gene_csvs_equal_the_reference(tmp_path, devices):
     """GatherCellAndGeneMetrics on the reference's unsorted.bam: the cell CSV is, byte for byte,

@@ -261,3 +261,60 @@ def test_tie_runs_of_every_length(eng):
     idx = np_order(arrays, "cell_umi_gene", tie)
     for c in N.RECORD_COLUMNS:
         assert np.array_equal(out[c], arrays[c][idx]), c
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_tie", [False, True])
+def test_group_sort_long_groups(eng, with_tie):
+    """Round 6 group sort (tagsort.h): groups of equal (cell, top umi bits) longer than a wave go to the
+    one-block-per-group LDS sort (65 .. 2048 records), the rest to the 64-lane networks -- all must give
+    numpy's stable lexsort by (CB, UB, GE[, query name]), ties in input order."""
+    from sctools_amd import engine as E
+
+    d, _, arrays = shuffled_synth(120_000, 12, n_cells=40)
+    arrays = {c: a.copy() for c, a in arrays.items()}
+    rng = np.random.default_rng(5)
+    n = arrays["cell"].shape[0]
+    for L in [63, 64, 65, 66, 100, 127, 128, 129, 300, 1000, 2048]:
+        idx = rng.choice(n, size=L, replace=False)
+        arrays["cell"][idx] = arrays["cell"][idx[0]]
+        arrays["umi"][idx] = arrays["umi"][idx[0]]  # genes stay random: sorted inside the group
+    tie = rng.integers(0, 50, n).astype(np.int32) if with_tie else None
+    dims = E.Dims(d.n_cell_ids, d.n_gene_ids, d.n_umi_ids)
+    out = to_host(eng.tag_sort(to_dev(eng, arrays), dims, "cell_umi_gene",
+                               None if tie is None else torch.from_numpy(tie).to(eng.device), 50))
+    idx = np_order(arrays, "cell_umi_gene", tie)
+    for c in N.RECORD_COLUMNS:
+        assert np.array_equal(out[c], arrays[c][idx]), c
+
+
+@pytest.mark.gpu
+def test_group_sort_equals_general_path(eng, monkeypatch):
+    """The group sort and the general path (7 LSD passes + run fix-up; SCT_TAG_GROUP_SORT=0) give the same
+    records on a config-5-shaped shuffled set, and fall back to the general path for a cell id the group
+    key cannot hold."""
+    from sctools_amd import engine as E
+    from sctools_amd import synth
+
+    cfg = synth.SynthConfig(n_reads=2_000_000, n_cells=200, n_genes=30_000, seed=13, p_secondary=0.1, p_nh1=0.7,
+                            p_dup=0.4)
+    data = synth.generate(cfg, device=eng.device)
+    perm = torch.randperm(cfg.n_reads, generator=torch.Generator().manual_seed(4)).to(eng.device)
+    cols = {c: t[perm].contiguous() for c, t in data.cols.items()}
+    tie = data.extra["qname"][perm].contiguous()
+    dims = E.Dims(data.n_cell_ids, data.n_gene_ids, data.n_umi_ids)
+    nq = data.extra["n_qnames"]
+    got = to_host(eng.tag_sort(cols, dims, "cell_umi_gene", tie, nq))
+    monkeypatch.setenv("SCT_TAG_GROUP_SORT", "0")
+    want = to_host(eng.tag_sort(cols, dims, "cell_umi_gene", tie, nq))
+    monkeypatch.delenv("SCT_TAG_GROUP_SORT")
+    for c in N.RECORD_COLUMNS:
+        assert np.array_equal(got[c], want[c]), c
+    # a cell id >= 2^bits(n_cell_ids): the general path's result (which keeps the id in its row)
+    bad = {c: t.clone() for c, t in cols.items()}
+    bad["cell"][17] = 1 << 20
+    got = to_host(eng.tag_sort(bad, dims, "cell_umi_gene", tie, nq))
+    monkeypatch.setenv("SCT_TAG_GROUP_SORT", "0")
+    want = to_host(eng.tag_sort(bad, dims, "cell_umi_gene", tie, nq))
+    for c in N.RECORD_COLUMNS:
+        assert np.array_equal(got[c], want[c]), c
