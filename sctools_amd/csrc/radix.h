@@ -29,7 +29,7 @@ static_assert(kRadix == kBlock, "digit-per-thread scan assumes kRadix == kBlock"
 
 // K: uint64_t, or uint32_t for keys of <= 32 bits (round 6: the group tag sort's K1 -- a third less
 // traffic per pass)
-template <typename K = uint64_t>
+template <typename K = uint64_t, int kIt = kSortItems>
 __global__ void k_radix_upsweep(const K* __restrict__ keys, int64_t n, int shift, int64_t num_tiles,
                                 uint32_t* __restrict__ counts) {
   __shared__ uint32_t hist[kWaves][kRadix];
@@ -37,9 +37,9 @@ __global__ void k_radix_upsweep(const K* __restrict__ keys, int64_t n, int shift
   for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&hist[0][0])[i] = 0;
   __syncthreads();
   const unsigned tile = xcd_tile(blockIdx.x, gridDim.x);  // consecutive tiles on one XCD
-  const int64_t base = (int64_t)tile * kSortTile;
+  const int64_t base = (int64_t)tile * (kBlock * kIt);
 #pragma unroll
-  for (int j = 0; j < kSortItems; j++) {
+  for (int j = 0; j < kIt; j++) {
     const int64_t p = base + (int64_t)j * kBlock + threadIdx.x;
     if (p < n) atomicAdd(&hist[wid][(keys[p] >> shift) & (kRadix - 1)], 1u);
   }
@@ -52,14 +52,16 @@ __global__ void k_radix_upsweep(const K* __restrict__ keys, int64_t n, int shift
   }
 }
 
-template <typename K = uint64_t>
+// kIdx: the values are the input positions (the first pass over freshly packed keys): not read
+template <typename K = uint64_t, bool kIdx = false, int kIt = kSortItems>
 __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const K* __restrict__ keys_in,
                                                             const uint32_t* __restrict__ vals_in,
                                                             K* __restrict__ keys_out,
                                                             uint32_t* __restrict__ vals_out, int64_t n, int shift,
                                                             int64_t num_tiles, const uint32_t* __restrict__ offsets) {
-  __shared__ K s_keys[kSortTile];
-  __shared__ uint32_t s_vals[kSortTile];
+  constexpr int kTileN = kBlock * kIt;
+  __shared__ K s_keys[kTileN];
+  __shared__ uint32_t s_vals[kTileN];
   __shared__ uint32_t s_whist[kWaves][kRadix];
   __shared__ uint32_t s_dstart[kRadix];
   __shared__ uint32_t s_goff[kRadix];  // this tile's output offset per digit (one global read each)
@@ -70,26 +72,26 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const K* __restrict_
   // consecutive tiles on one XCD: a digit's runs of neighbouring tiles are neighbours in the
   // output, so their partly written lines meet in that XCD's L2 instead of two L2s
   const unsigned tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int64_t base = (int64_t)tile * kSortTile;
-  const int tile_n = (int)((n - base) < kSortTile ? (n - base) : kSortTile);
+  const int64_t base = (int64_t)tile * kTileN;
+  const int tile_n = (int)((n - base) < kTileN ? (n - base) : kTileN);
 
   for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_whist[0][0])[i] = 0;
   s_goff[threadIdx.x] = offsets[(int64_t)threadIdx.x * num_tiles + tile];  // kRadix == kBlock
   __syncthreads();
 
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  K k[kSortItems];
-  uint32_t v[kSortItems];
-  uint16_t rank[kSortItems];
-  uint8_t dig[kSortItems];
-  // wave `wid` owns tile positions [wid*kSortItems*kWave, ...); round j covers 64 of them
+  K k[kIt];
+  uint32_t v[kIt];
+  uint16_t rank[kIt];
+  uint8_t dig[kIt];
+  // wave `wid` owns tile positions [wid*kIt*kWave, ...); round j covers 64 of them
 #pragma unroll
-  for (int j = 0; j < kSortItems; j++) {
-    const int q = wid * (kSortItems * kWave) + j * kWave + lane;
+  for (int j = 0; j < kIt; j++) {
+    const int q = wid * (kIt * kWave) + j * kWave + lane;
     const int64_t p = base + q;
     if (q < tile_n) {
       k[j] = keys_in[p];
-      v[j] = vals_in[p];
+      v[j] = kIdx ? (uint32_t)p : vals_in[p];
     } else {
       k[j] = (K)~0ull;  // padding: digit 255 at every shift, ranked after all real items, never written
       v[j] = 0;
@@ -130,7 +132,7 @@ __global__ void __launch_bounds__(kBlock) k_radix_downsweep(const K* __restrict_
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kSortItems; j++) {
+  for (int j = 0; j < kIt; j++) {
     const uint32_t lp = s_whist[wid][dig[j]] + rank[j];
     s_keys[lp] = k[j];
     s_vals[lp] = v[j];
@@ -383,11 +385,21 @@ inline int radix_sort(const SortBuffers& B, int64_t n, int bits, int* which, hip
   return SCT_OK;
 }
 
-// the same over 32-bit keys (bits <= 32) held in the key buffers (ka / kb reinterpreted)
-inline int radix_sort32(const SortBuffers& B, int64_t n, int bits, int* which, hipStream_t s) {
+// items per thread of radix_sort32's tiles: 32-bit keys halve the tile's key staging, so a tile of
+// 4096 items (16 per digit on average, against 8 at 2048) takes the LDS of a 2048-item 64-bit tile
+#ifndef SCT_SORT_ITEMS32
+#define SCT_SORT_ITEMS32 16
+#endif
+constexpr int kSortItems32 = SCT_SORT_ITEMS32;
+static_assert(kSortItems32 >= kSortItems, "radix_sort32's tile counts fit the workspace's count_cap");
+// the same over 32-bit keys (bits <= 32) held in the key buffers (ka / kb reinterpreted).
+// positions: the values are the input positions (nothing in va): the first pass takes them from
+// the index.
+inline int radix_sort32(const SortBuffers& B, int64_t n, int bits, int* which, hipStream_t s,
+                        bool positions = false) {
   if (bits > 32) return fail(SCT_EINVAL, "radix_sort32: %d key bits", bits);
   const int passes = (bits + kRadixBits - 1) / kRadixBits;
-  const int64_t tiles = cdiv(n, kSortTile);
+  const int64_t tiles = cdiv(n, kBlock * kSortItems32);
   if ((int64_t)kRadix * tiles > B.count_cap)
     return fail(SCT_EINVAL, "radix_sort32: %lld digit counts exceed the workspace's %lld", (long long)(kRadix * tiles),
                 (long long)B.count_cap);
@@ -400,12 +412,18 @@ inline int radix_sort32(const SortBuffers& B, int64_t n, int bits, int* which, h
     const uint32_t* vin = cur ? B.vb : B.va;
     uint32_t* kout = cur ? ka : kb;
     uint32_t* vout = cur ? B.va : B.vb;
-    LAUNCH_N("radix_upsweep", n, k_radix_upsweep<uint32_t>, dim3((unsigned)tiles), dim3(kBlock), s, kin, n, shift,
-             tiles, B.counts);
+    const bool pre = positions && ps == 0;
+    LAUNCH_N("radix_upsweep", n, (k_radix_upsweep<uint32_t, kSortItems32>), dim3((unsigned)tiles), dim3(kBlock), s,
+             kin, n, shift, tiles, B.counts);
     int rc = scan_counts(B.counts, (int64_t)kRadix * tiles, B.offsets, B.sums, s);
     if (rc) return rc;
-    LAUNCH_N("radix_downsweep", n, k_radix_downsweep<uint32_t>, dim3((unsigned)tiles), dim3(kBlock), s, kin, vin, kout,
-             vout, n, shift, tiles, (const uint32_t*)B.offsets);
+    if (pre) {
+      LAUNCH_N("radix_downsweep", n, (k_radix_downsweep<uint32_t, true, kSortItems32>), dim3((unsigned)tiles),
+               dim3(kBlock), s, kin, vin, kout, vout, n, shift, tiles, (const uint32_t*)B.offsets);
+    } else {
+      LAUNCH_N("radix_downsweep", n, (k_radix_downsweep<uint32_t, false, kSortItems32>), dim3((unsigned)tiles),
+               dim3(kBlock), s, kin, vin, kout, vout, n, shift, tiles, (const uint32_t*)B.offsets);
+    }
     cur ^= 1;
   }
   *which = cur;

@@ -1055,9 +1055,14 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
       uint32_t* tctl = at<uint32_t>(workspace, L.tctl);
       HIPCHK(hipMemsetAsync(tctl, 0, 4 * sizeof(uint32_t), s));
       LAUNCH_N("tag_group_keys", n, k_pack_group_keys, grid, dim3(kBlock), s, *in, n, gb, tiebreak, recs,
-               reinterpret_cast<uint32_t*>(B.ka), B.va, tctl);
+               reinterpret_cast<uint32_t*>(B.ka), tctl);
       int which = 0;
-      rc = radix_sort32(B, n, gb.c + gb.ub, &which, s);
+      const int kbits = gb.c + gb.ub;
+      if (kbits > 0) {
+        rc = radix_sort32(B, n, kbits, &which, s, true);
+      } else {  // one group: the values are the positions
+        LAUNCH("tag_group_iota", k_iota, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), s, B.va, n);
+      }
       if (rc) return rc;
       const uint32_t* keys = reinterpret_cast<const uint32_t*>(which ? B.kb : B.ka);
       const uint32_t* perm = which ? B.vb : B.va;
