@@ -69,8 +69,13 @@ ALG_BYTES = {
     "radix_onesweep": 24,    # (opt-in onesweep) read key 8 + value 4, write key 8 + value 4
     "radix_hist_all": 8,
     "tag_unpack": 64,        # gather the packed record (32), write the SoA columns (32)
-    "radix_downsweep": 24,   # global-sort path: read key 8 + value 4, write key 8 + value 4
-    "radix_upsweep": 8,
+    # config 5's sort (round 6): the 32-bit group keys (tagsort.h); the 64-bit general path's passes
+    # move 24 and 8 bytes instead, and the bench does not run them
+    "radix_downsweep": 16,   # read key 4 + value 4, write key 4 + value 4
+    "radix_upsweep": 4,      # read key 4
+    "tag_group_keys": 72,    # read the SoA record (32) + tiebreak (4), write the row (32) + group key (4)
+    "tag_group_wave": 72,    # read the group key (4) + the permutation (4), gather the row (32), write SoA (32)
+    "tag_group_long": 72,    # the same for the records of groups longer than a wave
     "reduce_sorted": 12,
     "heads": 4,              # read the entity column
     "welford": 10,
@@ -85,7 +90,9 @@ PMC_NAMES = {"build_keys": ["build_keys_run"], "heads": ["heads4", "heads"], "fi
              "tag_pack": ["pack"], "tag_keys": ["field_keys", "round_keys"], "tag_ties": ["tie_wave", "tie_wave2"],
              "tag_pack_keys": ["pack_field_keys"],
              "tag_long_keys": ["long_keys"], "tag_long_scatter": ["long_scatter"], "tag_unpack": ["unpack"],
-             "tag_row_hist": ["row_hist"], "tag_row_scatter": ["row_scatter"]}
+             "tag_row_hist": ["row_hist"], "tag_row_scatter": ["row_scatter"],
+             "tag_group_keys": ["pack_group_keys"], "tag_group_wave": ["group_wave"],
+             "tag_group_long": ["group_long"], "tag_group_iota": ["iota"]}
 
 
 def pmc_bytes_per_launch(d, name):
