@@ -74,6 +74,8 @@ ALG_BYTES = {
     "radix_downsweep": 16,   # read key 4 + value 4, write key 4 + value 4
     "radix_upsweep": 4,      # read key 4
     "tag_group_keys": 72,    # read the SoA record (32) + tiebreak (4), write the row (32) + group key (4)
+    "tag_group_hist": 8,     # read the cell and umi columns (the MSD digit of the group key)
+    "tag_group_msd": 72,     # the MSD pass: read the SoA record (32) + tiebreak (4), write the row (32) + key (4)
     "tag_group_wave": 72,    # read the group key (4) + the permutation (4), gather the row (32), write SoA (32)
     "tag_group_long": 72,    # the same for the records of groups longer than a wave
     "reduce_sorted": 12,
@@ -92,7 +94,9 @@ PMC_NAMES = {"build_keys": ["build_keys_run"], "heads": ["heads4", "heads"], "fi
              "tag_long_keys": ["long_keys"], "tag_long_scatter": ["long_scatter"], "tag_unpack": ["unpack"],
              "tag_row_hist": ["row_hist"], "tag_row_scatter": ["row_scatter"],
              "tag_group_keys": ["pack_group_keys"], "tag_group_wave": ["group_wave"],
-             "tag_group_long": ["group_long"], "tag_group_iota": ["iota"]}
+             "tag_group_long": ["group_long"], "tag_group_iota": ["iota"], "tag_group_hist": ["gmsd_hist"],
+             "tag_group_msd": ["gmsd_scatter"], "tag_group_plan": ["gseg_plan"],
+             "radix_upsweep": ["radix_upsweep", "gseg_upsweep"], "radix_downsweep": ["radix_downsweep", "gseg_downsweep"]}
 
 
 def pmc_bytes_per_launch(d, name):

@@ -720,7 +720,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
 
 // ---- tag sort ----
 struct SortLayout {
-  size_t recs, recs2, ka, kb, va, vb, counts, offsets, sums, bad, lka, lkb, lva, lvb, longs, tctl, total;
+  size_t recs, recs2, ka, kb, va, vb, counts, offsets, sums, bad, lka, lkb, lva, lvb, longs, tctl, gseg, total;
   int64_t count_cap;
 };
 
@@ -776,7 +776,10 @@ SortLayout sort_layout(int64_t n) {
   // then read its own output, and the downsweep wrote through garbage offsets (the illegal memory
   // access of the SCT_SORT_ITEMS=4 build).  radix_sort now also checks its capacity.
   const int64_t row_tiles = cdiv(n1, kRowTile), sort_tiles = cdiv(n1, kSortTile);
-  const int64_t tiles = row_tiles > sort_tiles ? row_tiles : sort_tiles;
+  int64_t tiles = row_tiles > sort_tiles ? row_tiles : sort_tiles;
+  const int64_t seg_tiles = cdiv(n1, kSegTile) + kRadix;  // the group sort's segmented passes (tagsort.h)
+  tiles = tiles > seg_tiles ? tiles : seg_tiles;
+  tiles = tiles > cdiv(n1, kMsdTile) ? tiles : cdiv(n1, kMsdTile);  // and its MSD pass
   const int64_t m = (int64_t)kRadix * tiles;
   L.count_cap = m;
   size_t off = 0;
@@ -802,6 +805,7 @@ SortLayout sort_layout(int64_t n) {
   L.lvb = take(sizeof(uint32_t) * (size_t)n1);
   L.longs = take(sizeof(uint4) * (size_t)(n1 / (kTieShort + 1) + 1));
   L.tctl = take(4 * sizeof(uint32_t));
+  L.gseg = take((3 * kRadix + 1) * sizeof(uint32_t));
   L.total = off;
   return L;
 }
@@ -1054,18 +1058,63 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
       uint4* longs = at<uint4>(workspace, L.longs);
       uint32_t* tctl = at<uint32_t>(workspace, L.tctl);
       HIPCHK(hipMemsetAsync(tctl, 0, 4 * sizeof(uint32_t), s));
-      LAUNCH_N("tag_group_keys", n, k_pack_group_keys, grid, dim3(kBlock), s, *in, n, gb, tiebreak, recs,
-               reinterpret_cast<uint32_t*>(B.ka), tctl);
       int which = 0;
       const int kbits = gb.c + gb.ub;
-      if (kbits > 0) {
-        rc = radix_sort32(B, n, kbits, &which, s, true);
-      } else {  // one group: the values are the positions
-        LAUNCH("tag_group_iota", k_iota, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), s, B.va, n);
+      const char* msd_env = getenv("SCT_TAG_GROUP_MSD");
+      const bool msd = kbits > kRadixBits && !(msd_env && msd_env[0] == '0');
+      const uint32_t* keys = nullptr;
+      const uint32_t* perm = nullptr;
+      if (msd) {
+        // rows written once in the order of K1's top digit, then the rest of K1 inside those buckets
+        const int sh_top = kbits - kRadixBits;
+        const int64_t mt = cdiv(n, kMsdTile);
+        const int64_t tmax = cdiv(n, kSegTile) + kRadix;
+        if ((int64_t)kRadix * mt > L.count_cap || (int64_t)kRadix * tmax > L.count_cap)
+          return fail(SCT_EINVAL, "group sort: digit counts exceed the workspace");
+        uint32_t* ka32 = reinterpret_cast<uint32_t*>(B.ka);
+        uint32_t* kb32 = reinterpret_cast<uint32_t*>(B.kb);
+        uint32_t* gseg = at<uint32_t>(workspace, L.gseg);
+        LAUNCH_N("tag_group_hist", n, k_gmsd_hist, dim3((unsigned)mt), dim3(kBlock), s, in->cell, in->umi, n, gb,
+                 sh_top, mt, B.counts, tctl);
+        rc = scan_counts(B.counts, (int64_t)kRadix * mt, B.offsets, B.sums, s);
+        if (rc) return rc;
+        LAUNCH_N("tag_group_msd", n, k_gmsd_scatter, dim3((unsigned)mt), dim3(kBlock), s, *in, tiebreak, n, gb, sh_top,
+                 mt, (const uint32_t*)B.offsets, recs, ka32);
+        LAUNCH("tag_group_plan", k_gseg_plan, dim3(1), dim3(kBlock), s, (const uint32_t*)B.offsets, mt, n, gseg);
+        const int passes = (sh_top + kRadixBits - 1) / kRadixBits;
+        int cur = 0;
+        for (int ps = 0; ps < passes; ps++) {
+          const uint32_t* kin = cur ? kb32 : ka32;
+          const uint32_t* vin = cur ? B.vb : B.va;
+          uint32_t* kout = cur ? ka32 : kb32;
+          uint32_t* vout = cur ? B.va : B.vb;
+          LAUNCH_N("radix_upsweep", n, k_gseg_upsweep, dim3((unsigned)tmax), dim3(kBlock), s, kin, ps * kRadixBits,
+                   (const uint32_t*)gseg, B.counts);
+          rc = scan_counts(B.counts, (int64_t)kRadix * tmax, B.offsets, B.sums, s);
+          if (rc) return rc;
+          if (ps == 0) {
+            LAUNCH_N("radix_downsweep", n, k_gseg_downsweep<true>, dim3((unsigned)tmax), dim3(kBlock), s, kin, vin,
+                     kout, vout, ps * kRadixBits, (const uint32_t*)gseg, (const uint32_t*)B.offsets);
+          } else {
+            LAUNCH_N("radix_downsweep", n, k_gseg_downsweep<false>, dim3((unsigned)tmax), dim3(kBlock), s, kin, vin,
+                     kout, vout, ps * kRadixBits, (const uint32_t*)gseg, (const uint32_t*)B.offsets);
+          }
+          cur ^= 1;
+        }
+        keys = cur ? kb32 : ka32;
+        perm = cur ? B.vb : B.va;
+      } else {
+        LAUNCH_N("tag_group_keys", n, k_pack_group_keys, grid, dim3(kBlock), s, *in, n, gb, tiebreak, recs,
+                 reinterpret_cast<uint32_t*>(B.ka), tctl);
+        if (kbits > 0) {
+          rc = radix_sort32(B, n, kbits, &which, s, true);
+        } else {  // one group: the values are the positions
+          LAUNCH("tag_group_iota", k_iota, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), s, B.va, n);
+        }
+        if (rc) return rc;
+        keys = reinterpret_cast<const uint32_t*>(which ? B.kb : B.ka);
+        perm = which ? B.vb : B.va;
       }
-      if (rc) return rc;
-      const uint32_t* keys = reinterpret_cast<const uint32_t*>(which ? B.kb : B.ka);
-      const uint32_t* perm = which ? B.vb : B.va;
       uint2* glong = reinterpret_cast<uint2*>(longs);
       LAUNCH_N("tag_group_wave", n, k_group_wave, grid, dim3(kBlock), s, keys, perm, (const uint4*)recs, n, gb, *out,
                glong, tctl);

@@ -305,11 +305,15 @@ def test_group_sort_equals_general_path(eng, monkeypatch):
     dims = E.Dims(data.n_cell_ids, data.n_gene_ids, data.n_umi_ids)
     nq = data.extra["n_qnames"]
     got = to_host(eng.tag_sort(cols, dims, "cell_umi_gene", tie, nq))
+    monkeypatch.setenv("SCT_TAG_GROUP_MSD", "0")  # the group sort without its MSD pass (LSD over all of K1)
+    got_lsd = to_host(eng.tag_sort(cols, dims, "cell_umi_gene", tie, nq))
+    monkeypatch.delenv("SCT_TAG_GROUP_MSD")
     monkeypatch.setenv("SCT_TAG_GROUP_SORT", "0")
     want = to_host(eng.tag_sort(cols, dims, "cell_umi_gene", tie, nq))
     monkeypatch.delenv("SCT_TAG_GROUP_SORT")
     for c in N.RECORD_COLUMNS:
         assert np.array_equal(got[c], want[c]), c
+        assert np.array_equal(got_lsd[c], want[c]), c
     # a cell id >= 2^bits(n_cell_ids): the general path's result (which keeps the id in its row)
     bad = {c: t.clone() for c, t in cols.items()}
     bad["cell"][17] = 1 << 20
