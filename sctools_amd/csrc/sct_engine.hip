@@ -777,9 +777,10 @@ SortLayout sort_layout(int64_t n) {
   // access of the SCT_SORT_ITEMS=4 build).  radix_sort now also checks its capacity.
   const int64_t row_tiles = cdiv(n1, kRowTile), sort_tiles = cdiv(n1, kSortTile);
   int64_t tiles = row_tiles > sort_tiles ? row_tiles : sort_tiles;
-  const int64_t seg_tiles = cdiv(n1, kSegTile) + kRadix;  // the group sort's segmented passes (tagsort.h)
+  const int64_t seg_tiles = cdiv(n1, kSegTile) + kMsdRadix;  // the group sort's segmented passes (tagsort.h)
   tiles = tiles > seg_tiles ? tiles : seg_tiles;
-  tiles = tiles > cdiv(n1, kMsdTile) ? tiles : cdiv(n1, kMsdTile);  // and its MSD pass
+  const int64_t msd_tiles = cdiv(n1, kMsdTile) * (kMsdRadix / kRadix);  // and its MSD pass (kMsdRadix digits)
+  tiles = tiles > msd_tiles ? tiles : msd_tiles;
   const int64_t m = (int64_t)kRadix * tiles;
   L.count_cap = m;
   size_t off = 0;
@@ -805,7 +806,7 @@ SortLayout sort_layout(int64_t n) {
   L.lvb = take(sizeof(uint32_t) * (size_t)n1);
   L.longs = take(sizeof(uint4) * (size_t)(n1 / (kTieShort + 1) + 1));
   L.tctl = take(4 * sizeof(uint32_t));
-  L.gseg = take((3 * kRadix + 1) * sizeof(uint32_t));
+  L.gseg = take((3 * kMsdRadix + 1) * sizeof(uint32_t));
   L.total = off;
   return L;
 }
@@ -1053,30 +1054,37 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
     const int ub_min = gb.u + gb.g + gb.t - 52 > 0 ? gb.u + gb.g + gb.t - 52 : 0;  // W fits 52 bits
     const int passes = (gb.c + ub_min + kRadixBits - 1) / kRadixBits;
     if (ub_min <= gb.u && passes <= 4) {
-      gb.ub = kRadixBits * passes - gb.c < gb.u ? kRadixBits * passes - gb.c : gb.u;  // fill the last digit
+      const char* msd_env = getenv("SCT_TAG_GROUP_MSD");
+      const bool msd = gb.c + ub_min > kRadixBits && !(msd_env && msd_env[0] == '0');
+      // K1 is filled to the width its passes sort anyway (smaller groups for free): LSD, whole 8-bit
+      // digits; MSD, the kMsdBits-bit top digit plus the fewest 8-bit segmented passes (<= 32 bits)
+      int kw = kRadixBits * passes;
+      if (msd) {
+        const int segp = gb.c + ub_min > kMsdBits ? (gb.c + ub_min - kMsdBits + kRadixBits - 1) / kRadixBits : 0;
+        kw = kMsdBits + kRadixBits * segp < 32 ? kMsdBits + kRadixBits * segp : 32;
+      }
+      gb.ub = kw - gb.c < gb.u ? kw - gb.c : gb.u;
       gb.ul = gb.u - gb.ub;
       uint4* longs = at<uint4>(workspace, L.longs);
       uint32_t* tctl = at<uint32_t>(workspace, L.tctl);
       HIPCHK(hipMemsetAsync(tctl, 0, 4 * sizeof(uint32_t), s));
       int which = 0;
       const int kbits = gb.c + gb.ub;
-      const char* msd_env = getenv("SCT_TAG_GROUP_MSD");
-      const bool msd = kbits > kRadixBits && !(msd_env && msd_env[0] == '0');
       const uint32_t* keys = nullptr;
       const uint32_t* perm = nullptr;
       if (msd) {
         // rows written once in the order of K1's top digit, then the rest of K1 inside those buckets
-        const int sh_top = kbits - kRadixBits;
+        const int sh_top = kbits > kMsdBits ? kbits - kMsdBits : 0;
         const int64_t mt = cdiv(n, kMsdTile);
-        const int64_t tmax = cdiv(n, kSegTile) + kRadix;
-        if ((int64_t)kRadix * mt > L.count_cap || (int64_t)kRadix * tmax > L.count_cap)
+        const int64_t tmax = cdiv(n, kSegTile) + kMsdRadix;
+        if ((int64_t)kMsdRadix * mt > L.count_cap || (int64_t)kRadix * tmax > L.count_cap)
           return fail(SCT_EINVAL, "group sort: digit counts exceed the workspace");
         uint32_t* ka32 = reinterpret_cast<uint32_t*>(B.ka);
         uint32_t* kb32 = reinterpret_cast<uint32_t*>(B.kb);
         uint32_t* gseg = at<uint32_t>(workspace, L.gseg);
         LAUNCH_N("tag_group_hist", n, k_gmsd_hist, dim3((unsigned)mt), dim3(kBlock), s, in->cell, in->umi, n, gb,
                  sh_top, mt, B.counts, tctl);
-        rc = scan_counts(B.counts, (int64_t)kRadix * mt, B.offsets, B.sums, s);
+        rc = scan_counts(B.counts, (int64_t)kMsdRadix * mt, B.offsets, B.sums, s);
         if (rc) return rc;
         LAUNCH_N("tag_group_msd", n, k_gmsd_scatter, dim3((unsigned)mt), dim3(kBlock), s, *in, tiebreak, n, gb, sh_top,
                  mt, (const uint32_t*)B.offsets, recs, ka32);
@@ -1103,6 +1111,8 @@ int sct_tag_sort(const sct_plan_t* plan, const sct_records_t* in, const int32_t*
         }
         keys = cur ? kb32 : ka32;
         perm = cur ? B.vb : B.va;
+        if (passes == 0)  // the top digit was all of K1: the rows are in K1 order already
+          LAUNCH("tag_group_iota", k_iota, dim3((unsigned)cdiv(n, kBlock)), dim3(kBlock), s, B.va, n);
       } else {
         LAUNCH_N("tag_group_keys", n, k_pack_group_keys, grid, dim3(kBlock), s, *in, n, gb, tiebreak, recs,
                  reinterpret_cast<uint32_t*>(B.ka), tctl);

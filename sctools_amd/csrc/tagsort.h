@@ -598,13 +598,18 @@ __global__ void __launch_bounds__(kBlock) k_iota(uint32_t* __restrict__ v, int64
 // The group sort's last step gathers every record's 32-byte row at random; measured at config 5 it
 // took 3.9 ms on rows in input order and 2.6 ms on rows pre-grouped by the top bits of the cell
 // (tools/c5_locality_probe.py): the rows that consecutive output positions gather then share cache
-// lines and MALL residency.  So the rows are written once in the order of K1's top 8 bits (a stable
-// multi-split, rows staged in LDS per 2048-record tile, as k_row_scatter), and the rest of K1 is
+// lines and MALL residency.  So the rows are written once in the order of K1's top kMsdBits bits (a
+// stable multi-split, rows staged in LDS per 2048-record tile, as k_row_scatter), and the rest of K1 is
 // sorted by LSD passes INSIDE those buckets (segmented: each tile belongs to one bucket, and the
 // count matrix is laid out bucket-major, so one device-wide scan gives every bucket its own digit
-// offsets) -- one pass fewer than sorting all of K1.
+// offsets) -- one pass fewer than sorting all of K1.  The top digit is 9 bits wide (512 buckets), so
+// a 25-bit K1 -- config 5's (14-bit cell, 11 umi bits) -- takes two 8-bit segmented passes, not three.
 constexpr int kMsdItems = 8;
 constexpr int kMsdTile = kBlock * kMsdItems;  // 2048 records: 64 KB of rows + 8 KB of tiebreaks in LDS
+constexpr int kMsdBits = 9;
+constexpr int kMsdRadix = 1 << kMsdBits;  // buckets of the MSD pass
+static_assert(kMsdRadix == 2 * kBlock, "two top digits per thread");
+static_assert(kMsdTile <= 0xffff, "16-bit per-tile digit counts and starts");
 constexpr int kSegItems = 16;
 constexpr int kSegTile = kBlock * kSegItems;  // segmented LSD tiles (4096 items)
 
@@ -617,9 +622,9 @@ __device__ __forceinline__ uint32_t group_key(uint32_t cell, uint32_t umi, const
 __global__ void __launch_bounds__(kBlock) k_gmsd_hist(const int32_t* __restrict__ cell, const int32_t* __restrict__ umi,
                                                       int64_t n, GroupBits gb, int sh_top, int64_t tiles,
                                                       uint32_t* __restrict__ counts, uint32_t* __restrict__ ctl) {
-  __shared__ uint32_t hist[kWaves][kRadix];
+  __shared__ uint32_t hist[kWaves][kMsdRadix];
   const int wid = threadIdx.x / kWave;
-  for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&hist[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kWaves * kMsdRadix; i += kBlock) (&hist[0][0])[i] = 0;
   __syncthreads();
   const unsigned tile = xcd_tile(blockIdx.x, gridDim.x);
   const int64_t base = (int64_t)tile * kMsdTile;
@@ -630,48 +635,51 @@ __global__ void __launch_bounds__(kBlock) k_gmsd_hist(const int32_t* __restrict_
     if (p < n) {
       const uint32_t c = (uint32_t)cell[p];
       bad |= low_bits(c, gb.c) != c;
-      atomicAdd(&hist[wid][(group_key(c, (uint32_t)umi[p], gb) >> sh_top) & (kRadix - 1)], 1u);
+      atomicAdd(&hist[wid][(group_key(c, (uint32_t)umi[p], gb) >> sh_top) & (kMsdRadix - 1)], 1u);
     }
   }
   if (bad) atomicOr(&ctl[2], 1u);
   __syncthreads();
-  const int d = threadIdx.x;
-  uint32_t t = 0;
+  for (int d = threadIdx.x; d < kMsdRadix; d += kBlock) {
+    uint32_t t = 0;
 #pragma unroll
-  for (int w = 0; w < kWaves; w++) t += hist[w][d];
-  counts[(int64_t)d * tiles + tile] = t;
+    for (int w = 0; w < kWaves; w++) t += hist[w][d];
+    counts[(int64_t)d * tiles + tile] = t;
+  }
 }
 
 // the stable multi-split by the top digit: SoA columns + tiebreak in, rows (tiebreak in the cell's
-// word) + group keys out, each digit's records of the tile written as one run (k_row_scatter's scheme)
+// word) + group keys out, each digit's records of the tile written as one run (k_row_scatter's scheme).
+// Per-tile counts and starts are 16-bit (<= kMsdTile), so the 512 digits' bookkeeping takes 7 KB and
+// two blocks still share a CU's 160 KB of LDS.
 __global__ void __launch_bounds__(kBlock) k_gmsd_scatter(sct_records_t in, const int32_t* __restrict__ tie, int64_t n,
                                                          GroupBits gb, int sh_top, int64_t tiles,
                                                          const uint32_t* __restrict__ offsets,
                                                          uint4* __restrict__ rows_out, uint32_t* __restrict__ keys_out) {
   __shared__ uint4 s_rows[2 * kMsdTile];
   __shared__ uint32_t s_tie[kMsdTile];
-  __shared__ uint32_t s_whist[kWaves][kRadix];
-  __shared__ uint32_t s_dstart[kRadix];
-  __shared__ uint32_t s_goff[kRadix];
+  __shared__ uint16_t s_whist[kWaves][kMsdRadix];
+  __shared__ uint16_t s_dstart[kMsdRadix];
+  __shared__ uint32_t s_goff[kMsdRadix];
   __shared__ uint64_t s_scan[kWaves + 1];
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x / kWave;
   const unsigned tile = xcd_tile(blockIdx.x, gridDim.x);
   const int64_t base = (int64_t)tile * kMsdTile;
   const int tile_n = (int)((n - base) < kMsdTile ? (n - base) : kMsdTile);
-  for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_whist[0][0])[i] = 0;
-  s_goff[threadIdx.x] = offsets[(int64_t)threadIdx.x * tiles + tile];
+  for (int i = threadIdx.x; i < kWaves * kMsdRadix; i += kBlock) (&s_whist[0][0])[i] = 0;
+  for (int d = threadIdx.x; d < kMsdRadix; d += kBlock) s_goff[d] = offsets[(int64_t)d * tiles + tile];
   __syncthreads();
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
   uint4 ra[kMsdItems], rb[kMsdItems];
   uint32_t tv[kMsdItems];
   uint16_t rank[kMsdItems];
-  uint8_t dig[kMsdItems];
+  uint16_t dig[kMsdItems];
 #pragma unroll
   for (int j = 0; j < kMsdItems; j++) {
     const int q = wid * (kMsdItems * kWave) + j * kWave + lane;
     const int64_t p = base + q;
-    uint32_t d = kRadix - 1;  // padding ranks last and is never written
+    uint32_t d = kMsdRadix - 1;  // padding ranks last and is never written
     if (q < tile_n) {
       ra[j] = make_uint4((uint32_t)in.cell[p], (uint32_t)in.umi[p], (uint32_t)in.gene[p], (uint32_t)in.ref[p]);
       rb[j] = make_uint4((uint32_t)in.pos[p], (uint32_t)in.gq_sum[p] | ((uint32_t)in.gq_len[p] << 16),
@@ -679,12 +687,12 @@ __global__ void __launch_bounds__(kBlock) k_gmsd_scatter(sct_records_t in, const
                          (uint32_t)in.cy_gt30[p] | ((uint32_t)in.cy_len[p] << 8) | ((uint32_t)in.uy_gt30[p] << 16) |
                              ((uint32_t)in.uy_len[p] << 24));
       tv[j] = tie ? (uint32_t)tie[p] : 0u;
-      d = (group_key(ra[j].x, ra[j].y, gb) >> sh_top) & (kRadix - 1);
+      d = (group_key(ra[j].x, ra[j].y, gb) >> sh_top) & (kMsdRadix - 1);
     }
-    dig[j] = (uint8_t)d;
+    dig[j] = (uint16_t)d;
     uint64_t peers = ~0ull;
 #pragma unroll
-    for (int bitn = 0; bitn < kRadixBits; bitn++) {
+    for (int bitn = 0; bitn < kMsdBits; bitn++) {
       const uint64_t m = __ballot((d >> bitn) & 1u);
       peers &= ((d >> bitn) & 1u) ? m : ~m;
     }
@@ -693,33 +701,41 @@ __global__ void __launch_bounds__(kBlock) k_gmsd_scatter(sct_records_t in, const
     uint32_t bse = 0;
     if (lane == leader) {
       bse = s_whist[wid][d];
-      s_whist[wid][d] = bse + (uint32_t)__popcll(peers);
+      s_whist[wid][d] = (uint16_t)(bse + (uint32_t)__popcll(peers));
     }
     bse = (uint32_t)__shfl((int)bse, leader);
     rank[j] = (uint16_t)(bse + below);
   }
   __syncthreads();
   {
-    const int d = threadIdx.x;
-    uint32_t run = 0;
-    uint32_t pre[kWaves];
+    // thread t: digits 2t and 2t + 1
+    const int d0 = 2 * threadIdx.x, d1 = d0 + 1;
+    uint32_t run0 = 0, run1 = 0;
+    uint32_t pre0[kWaves], pre1[kWaves];
 #pragma unroll
     for (int w = 0; w < kWaves; w++) {
-      pre[w] = run;
-      run += s_whist[w][d];
+      pre0[w] = run0;
+      run0 += s_whist[w][d0];
+      pre1[w] = run1;
+      run1 += s_whist[w][d1];
     }
     uint64_t tot;
-    const uint64_t ds = block_exclusive_scan<uint64_t>((uint64_t)run, &tot, s_scan);
-    s_dstart[d] = (uint32_t)ds;
+    const uint32_t ds0 = (uint32_t)block_exclusive_scan<uint64_t>((uint64_t)(run0 + run1), &tot, s_scan);
+    const uint32_t ds1 = ds0 + run0;
+    s_dstart[d0] = (uint16_t)ds0;
+    s_dstart[d1] = (uint16_t)ds1;
 #pragma unroll
-    for (int w = 0; w < kWaves; w++) s_whist[w][d] = (uint32_t)ds + pre[w];
+    for (int w = 0; w < kWaves; w++) {
+      s_whist[w][d0] = (uint16_t)(ds0 + pre0[w]);
+      s_whist[w][d1] = (uint16_t)(ds1 + pre1[w]);
+    }
   }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kMsdItems; j++) {
     const int q = wid * (kMsdItems * kWave) + j * kWave + lane;
     if (q < tile_n) {
-      const uint32_t lp = s_whist[wid][dig[j]] + rank[j];
+      const uint32_t lp = (uint32_t)s_whist[wid][dig[j]] + rank[j];
       s_rows[2 * lp] = ra[j];
       s_rows[2 * lp + 1] = rb[j];
       s_tie[lp] = tv[j];
@@ -730,7 +746,7 @@ __global__ void __launch_bounds__(kBlock) k_gmsd_scatter(sct_records_t in, const
     const uint4 a = s_rows[2 * q];
     const uint4 b = s_rows[2 * q + 1];
     const uint32_t k = group_key(a.x, a.y, gb);
-    const uint32_t d = (k >> sh_top) & (kRadix - 1);
+    const uint32_t d = (k >> sh_top) & (kMsdRadix - 1);
     const uint64_t o = (uint64_t)s_goff[d] + (uint32_t)(q - (int)s_dstart[d]);
     rows_out[2 * o] = make_uint4(s_tie[q], a.y, a.z, a.w);
     rows_out[2 * o + 1] = b;
@@ -739,21 +755,29 @@ __global__ void __launch_bounds__(kBlock) k_gmsd_scatter(sct_records_t in, const
 }
 
 // one block: the buckets (digits of the MSD pass) -> their starts, sizes and first segmented tile
-// (gseg[0..255] start, [256..511] size, [512..768] tile base incl. the total at 768)
+// (gseg[0, R) start, [R, 2R) size, [2R, 3R) tile base, gseg[3R] the tile total; R = kMsdRadix)
 __global__ void __launch_bounds__(kBlock) k_gseg_plan(const uint32_t* __restrict__ offsets, int64_t tiles, int64_t n,
                                                       uint32_t* __restrict__ gseg) {
   __shared__ uint64_t s_scan[kWaves + 1];
-  const int d = threadIdx.x;
-  const uint32_t st = offsets[(int64_t)d * tiles];
-  const uint32_t nx = d + 1 < kRadix ? offsets[(int64_t)(d + 1) * tiles] : (uint32_t)n;
-  const uint32_t sz = nx - st;
-  const uint32_t nt = (sz + kSegTile - 1) / kSegTile;
+  uint32_t st[2], sz[2], nt[2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int d = 2 * threadIdx.x + i;
+    st[i] = offsets[(int64_t)d * tiles];
+    const uint32_t nx = d + 1 < kMsdRadix ? offsets[(int64_t)(d + 1) * tiles] : (uint32_t)n;
+    sz[i] = nx - st[i];
+    nt[i] = (sz[i] + kSegTile - 1) / kSegTile;
+  }
   uint64_t tot;
-  const uint64_t tb = block_exclusive_scan<uint64_t>((uint64_t)nt, &tot, s_scan);
-  gseg[d] = st;
-  gseg[kRadix + d] = sz;
-  gseg[2 * kRadix + d] = (uint32_t)tb;
-  if (d == 0) gseg[3 * kRadix] = (uint32_t)tot;
+  const uint32_t tb0 = (uint32_t)block_exclusive_scan<uint64_t>((uint64_t)(nt[0] + nt[1]), &tot, s_scan);
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int d = 2 * threadIdx.x + i;
+    gseg[d] = st[i];
+    gseg[kMsdRadix + d] = sz[i];
+    gseg[2 * kMsdRadix + d] = tb0 + (i ? nt[0] : 0u);
+  }
+  if (threadIdx.x == 0) gseg[3 * kMsdRadix] = (uint32_t)tot;
 }
 
 // a segmented tile's bucket and range: tile base b = the last bucket whose first tile <= tile
@@ -763,26 +787,26 @@ struct SegTile {
   int64_t base;
   int len;
 };
-// (tb: the bucket tile bases, gseg[512..768], staged in LDS by the caller: seg_stage)
+// (tb: the bucket tile bases, gseg[2R .. 3R], staged in LDS by the caller: seg_stage)
 __device__ __forceinline__ const uint32_t* seg_stage(const uint32_t* __restrict__ gseg, uint32_t* s_tb) {
-  s_tb[threadIdx.x] = gseg[2 * kRadix + threadIdx.x];  // kRadix == kBlock
-  if (threadIdx.x == 0) s_tb[kRadix] = gseg[3 * kRadix];
+  for (int d = threadIdx.x; d < kMsdRadix; d += kBlock) s_tb[d] = gseg[2 * kMsdRadix + d];
+  if (threadIdx.x == 0) s_tb[kMsdRadix] = gseg[3 * kMsdRadix];
   __syncthreads();
   return s_tb;
 }
 __device__ __forceinline__ bool seg_tile(const uint32_t* __restrict__ gseg, const uint32_t* tb, uint32_t tile,
                                          SegTile& st) {
-  if (tile >= tb[kRadix]) return false;
-  int lo = 0, hi = kRadix - 1;  // the last b with tb[b] <= tile (empty buckets share their successor's base)
+  if (tile >= tb[kMsdRadix]) return false;
+  int lo = 0, hi = kMsdRadix - 1;  // the last b with tb[b] <= tile (empty buckets share their successor's base)
   while (lo < hi) {
     const int mid = (lo + hi + 1) / 2;
     if (tb[mid] <= tile) lo = mid; else hi = mid - 1;
   }
   st.b = lo;
   st.tl = tile - tb[lo];
-  st.nt = (lo + 1 < kRadix ? tb[lo + 1] : tb[kRadix]) - tb[lo];
+  st.nt = (lo + 1 < kMsdRadix ? tb[lo + 1] : tb[kMsdRadix]) - tb[lo];
   st.base = (int64_t)gseg[lo] + (int64_t)st.tl * kSegTile;
-  const int64_t rem = (int64_t)gseg[kRadix + lo] - (int64_t)st.tl * kSegTile;
+  const int64_t rem = (int64_t)gseg[kMsdRadix + lo] - (int64_t)st.tl * kSegTile;
   st.len = (int)(rem < kSegTile ? rem : kSegTile);
   return true;
 }
@@ -795,7 +819,7 @@ __global__ void __launch_bounds__(kBlock) k_gseg_upsweep(const uint32_t* __restr
                                                          const uint32_t* __restrict__ gseg,
                                                          uint32_t* __restrict__ counts) {
   __shared__ uint32_t hist[kWaves][kRadix];
-  __shared__ uint32_t s_tb[kRadix + 1];
+  __shared__ uint32_t s_tb[kMsdRadix + 1];
   const uint32_t* tb = seg_stage(gseg, s_tb);
   SegTile st;
   // consecutive tiles on one XCD (radix.h): their digit runs' partly written lines meet in one L2
@@ -830,8 +854,10 @@ __global__ void __launch_bounds__(kBlock) k_gseg_downsweep(const uint32_t* __res
   __shared__ uint32_t s_dstart[kRadix];
   __shared__ uint32_t s_goff[kRadix];
   __shared__ uint64_t s_scan[kWaves + 1];
-  __shared__ uint32_t s_tb[kRadix + 1];
-  const uint32_t* tb = seg_stage(gseg, s_tb);
+  // the bucket tile bases are staged in s_vals: read only before the barrier after s_goff (s_vals is
+  // written two barriers later), so the block stays at 40 KB of LDS, 4 blocks per CU
+  static_assert(kSegTile >= kMsdRadix + 1, "tile bases fit s_vals");
+  const uint32_t* tb = seg_stage(gseg, s_vals);
   SegTile st;
   // consecutive tiles on one XCD (radix.h): their digit runs' partly written lines meet in one L2
   if (!seg_tile(gseg, tb, xcd_tile(blockIdx.x, gridDim.x), st)) return;  // block-uniform

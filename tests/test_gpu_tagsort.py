@@ -289,6 +289,30 @@ def test_group_sort_long_groups(eng, with_tie):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_cell_ids,n_umi_ids,n_gene_ids,n_tie", [
+    (32, 1 << 12, 1 << 16, 1 << 28),         # K1 of 9 bits: the MSD digit is all of it (no segmented pass)
+    (512, 1 << 12, 1 << 16, 1 << 28),        # 17 bits: one segmented pass
+    (1 << 14, 1 << 20, 1 << 16, 1 << 28),    # 32 bits: the top digit at bit 23, three segmented passes
+])
+def test_group_sort_key_widths(eng, n_cell_ids, n_umi_ids, n_gene_ids, n_tie):
+    """The group sort's 9-bit MSD digit with 0, 1 and 3 segmented 8-bit passes below it (sct_tag_sort
+    picks the group key's width from the dictionary sizes: tests/test_group_sort_cpu.py) gives numpy's
+    stable lexsort by (CB, UB, GE, query name)."""
+    from sctools_amd import engine as E
+
+    _, _, arrays = shuffled_synth(150_000, 14, n_cells=min(300, n_cell_ids - 2))
+    arrays = {c: a.copy() for c, a in arrays.items()}
+    arrays["umi"] %= min(n_umi_ids, 64)  # few umis: long groups and equal keys
+    n = arrays["cell"].shape[0]
+    tie = np.random.default_rng(6).integers(0, 1000, n).astype(np.int32)
+    dims = E.Dims(n_cell_ids, n_gene_ids, n_umi_ids)
+    out = to_host(eng.tag_sort(to_dev(eng, arrays), dims, "cell_umi_gene", torch.from_numpy(tie).to(eng.device), n_tie))
+    idx = np_order(arrays, "cell_umi_gene", tie)
+    for c in N.RECORD_COLUMNS:
+        assert np.array_equal(out[c], arrays[c][idx]), c
+
+
+@pytest.mark.gpu
 def test_group_sort_equals_general_path(eng, monkeypatch):
     """The group sort and the general path (7 LSD passes + run fix-up; SCT_TAG_GROUP_SORT=0) give the same
     records on a config-5-shaped shuffled set, and fall back to the general path for a cell id the group
