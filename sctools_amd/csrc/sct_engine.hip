@@ -274,9 +274,24 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
            n, bdesc, bent, seg[0], work[0], bigs, ctl, &ctl->n_seg);
   }
   BucketCtl h{};
-  if (int rb = readback(&h, ctl, sizeof(h), s)) return rb;
-  if (h.err & 2) return fail(SCT_EINVAL, "a gene / cell / umi id lies outside its dictionary size");
-  if (h.err) return 1;
+  // planned: the level-1 counts were read back early (pipeline: queued before the key pass), so the
+  // host sizes level 2 while the key pass still runs; the key pass's error flag is read with the next
+  // level's counts (kernels before that stay in bounds: ids are clamped, ref ids masked)
+  bool err_pending = false;
+  if (planned) {
+    if (int rb = readback_finish(&h, sizeof(h))) return rb;
+    err_pending = true;
+  }
+  if (!planned || h.n_seg == 0) {
+    if (int rb = readback(&h, ctl, sizeof(h), s)) return rb;
+    err_pending = false;
+  }
+  const auto err_check = [&]() -> int {
+    if (h.err & 2) return fail(SCT_EINVAL, "a gene / cell / umi id lies outside its dictionary size");
+    return h.err ? 1 : SCT_OK;
+  };
+  if (!err_pending)
+    if (int e = err_check()) return e;
   while (h.n_seg > 0) {
     if ((int64_t)h.n_seg > L.max_seg || (int64_t)h.n_work > L.max_work)
       return fail(SCT_ENOMEM, "bucket level %d: %u segments / %u work items exceed the workspace", level, h.n_seg,
@@ -299,6 +314,10 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     LAUNCH("bucket_scatter", k_bucket_scatter, dim3(n_work), dim3(kSBlock), s, pin, pout,
            (const Seg*)seg[c], (const Work*)work[c], shift, bits, cur);
     if (int rb = readback_finish(&h, sizeof(h))) return rb;
+    if (err_pending) {
+      err_pending = false;
+      if (int e = err_check()) return e;
+    }
     c ^= 1;
     depth += bits;
     level++;
@@ -623,6 +642,9 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   if (planned) {
     rc = bucket_level1_plan(L, ws, kc, n, n_ent, b, ent_start, l1, s);
     if (rc) return rc;
+    // level 1's counts, final after its classification: copied now, read by bucket_distinct while
+    // the key pass runs (no host wait between the key pass and level 2)
+    if (int rb = readback_start(bucket_ctl(ws, L), sizeof(BucketCtl), s)) return rb;
   }
   // Welford (the drop-in default): forked as soon as the entity starts exist -- after the level-1
   // plan when there is one (round 4: the head group's chains then start before the key pass),
