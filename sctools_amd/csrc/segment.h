@@ -467,11 +467,18 @@ __device__ __forceinline__ void stream_tile(const RecCols& r, int64_t base, int 
 #pragma unroll
       for (int j = 0; j < kItems; j++) sample(j);
     } else {
+      // a run boundary inside the thread's own items: only this thread's lanes change runs, so it
+      // adds them to the ending run's row by itself (8 atomics, no wave-wide reduction per item)
 #pragma unroll
       for (int j = 0; j < kItems; j++) {
-        const bool hd = (ch >> j) & 1u;
-        wave_flush<kStreamLanes>(lanes, hd, cur_e, partials, slot);
-        if (hd) cur_e += 1;
+        if ((ch >> j) & 1u) {
+#pragma unroll
+          for (int i = 0; i < kStreamLanes; i++) {
+            atomicAdd((unsigned long long*)&partials[cur_e * SCT_NP + slot(i)], (unsigned long long)lanes[i]);
+            lanes[i] = 0;
+          }
+          cur_e += 1;
+        }
         sample(j);
       }
     }
