@@ -238,6 +238,63 @@ int bucket_level1_plan(const Layout& L, void* ws, const KeyCols& kc, int64_t n, 
   return SCT_OK;
 }
 
+// One stream of the device's side-stream pool (below) for work beside the caller's stream (round 6):
+// from_caller() makes it wait for the work queued on the caller's stream so far, to_caller() the
+// reverse; use() hands out the stream for a launch.
+hipError_t side_streams(int dev, hipStream_t* s2, hipStream_t* s3, bool* alone);
+void side_streams_release(int dev, hipStream_t s2, hipStream_t s3);
+struct SideStream {
+  int dev = -1;
+  hipStream_t s = nullptr, s_pair = nullptr;
+  std::vector<hipEvent_t> evs;
+  bool synced = true;  // the caller's stream waits for everything queued here so far
+  bool is_open() const { return s != nullptr; }
+  hipError_t open(hipStream_t caller) {
+    if (s) return from_caller(caller);
+    int prev = 0;
+    hipError_t e = hipStreamGetDevice(caller, &dev);
+    if (e == hipSuccess) e = hipGetDevice(&prev);
+    if (e != hipSuccess) return e;
+    if (prev != dev && (e = hipSetDevice(dev)) != hipSuccess) return e;
+    bool alone = true;
+    e = side_streams(dev, &s, &s_pair, &alone);
+    if (e != hipSuccess) s = nullptr;
+    if (prev != dev) (void)hipSetDevice(prev);
+    return e == hipSuccess ? from_caller(caller) : e;
+  }
+  hipStream_t use() {
+    synced = false;
+    return s;
+  }
+  hipError_t event(hipEvent_t* ev) {
+    hipError_t e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    if (e == hipSuccess) evs.push_back(*ev);
+    return e;
+  }
+  hipError_t from_caller(hipStream_t caller) {
+    hipEvent_t ev = nullptr;
+    hipError_t e = event(&ev);
+    if (e == hipSuccess) e = hipEventRecord(ev, caller);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
+    return e;
+  }
+  hipError_t to_caller(hipStream_t caller) {
+    hipEvent_t ev = nullptr;
+    hipError_t e = event(&ev);
+    if (e == hipSuccess) e = hipEventRecord(ev, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(caller, ev, 0);
+    if (e == hipSuccess) synced = true;
+    return e;
+  }
+  ~SideStream() {
+    // an early return (an error, or the global-sort redo that reuses the workspace): nothing may
+    // still write into the workspace once the call is left
+    if (s && !synced) (void)hipStreamSynchronize(s);
+    for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
+    if (s) side_streams_release(dev, s, s_pair);
+  }
+};
+
 // bucket.h driver: level 0 classification, MSD levels until no segment exceeds kBCap, then
 // the hash-tile pass (+ giants).  One host wait per level to size the next level's launches,
 // for a copy queued right after the classification: the level's scatter runs meanwhile.
@@ -247,7 +304,7 @@ int bucket_level1_plan(const Layout& L, void* ws, const KeyCols& kc, int64_t n, 
 // the caller then reruns on the global-sort path.
 int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const int64_t* ent_start,
                     const uint8_t* mito, const Bits& b, bool cell, bool gene, int64_t* partials, uint16_t* dflags,
-                    bool planned, hipStream_t s) {
+                    bool planned, hipStream_t s, SideStream& side) {
   if (n == 0) return SCT_OK;
   Pay* pa = at<Pay>(ws, L.pay_a);
   Pay* pb = at<Pay>(ws, L.pay_b);
@@ -292,6 +349,33 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   };
   if (!err_pending)
     if (int e = err_check()) return e;
+  // Round 6: the big buckets of levels 0 and 1 (their records are final once the key pass has run)
+  // start on a side stream right away, beside levels >= 2, whose small partition kernels leave most
+  // CUs idle; the caller's stream waits for them after the hash-tile launch.  Big buckets, level
+  // segments and terminal buckets are disjoint record ranges, and the partial rows are summed
+  // with atomics, so the order between the streams does not matter.
+  const auto launch_big = [&](uint32_t cnt, const Seg* bg, hipStream_t st) -> int {
+    const dim3 bgrid(cnt);
+    const bool wide = b.k1 > kNarrowK1Bits;
+#define SCT_BIG(C, G, W) \
+  LAUNCH("big_bucket", (k_big_bucket<C, G, W>), bgrid, dim3(kBigBlock), st, bg, pa, pb, b, partials, dflags)
+    if (cell && gene) {
+      if (wide) { SCT_BIG(true, true, true); } else { SCT_BIG(true, true, false); }
+    } else if (cell) {
+      if (wide) { SCT_BIG(true, false, true); } else { SCT_BIG(true, false, false); }
+    } else {
+      if (wide) { SCT_BIG(false, false, true); } else { SCT_BIG(false, false, false); }
+    }
+#undef SCT_BIG
+    return SCT_OK;
+  };
+  const char* no_early = getenv("SCT_NO_EARLY_BIG");
+  const bool early_big = side.is_open() && h.n_big > 0 && h.n_seg > 0 && !(no_early && no_early[0] == '1');
+  uint32_t big_done = 0;
+  if (early_big) {
+    if (int r = launch_big(h.n_big, bigs, side.use())) return r;
+    big_done = h.n_big;
+  }
   while (h.n_seg > 0) {
     if ((int64_t)h.n_seg > L.max_seg || (int64_t)h.n_work > L.max_work)
       return fail(SCT_ENOMEM, "bucket level %d: %u segments / %u work items exceed the workspace", level, h.n_seg,
@@ -323,6 +407,11 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     level++;
   }
   const dim3 tgrid((unsigned)cdiv(n, kWin));
+  // the early big buckets finish before the hash tiles start (SCT_BIG_BESIDE_HASH=1: they may run into
+  // them; the hash tiles' 40 KB blocks then hold every CU's LDS and the big buckets' 80 KB blocks wait)
+  const char* beside = getenv("SCT_BIG_BESIDE_HASH");
+  const bool join_first = early_big && !(beside && beside[0] == '1');
+  if (join_first) HIPCHK(side.to_caller(s));
   int rc;
   if (b.k1 > kNarrowK1Bits) {
     rc = launch_hash_tile<true>(cell, gene, tgrid, s, bdesc, bent, pa, pb, n, b, partials, dflags);
@@ -331,21 +420,12 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   }
   if (rc) return rc;
   // (round 4: the big buckets on a side stream beside the hash tiles measured the same step time,
-  // 5.26 ms either way, profiles/r04/e_l1fast_gbam_dicts/var/)
-  if (h.n_big > 0) {
-    const dim3 bgrid(h.n_big);
-    const bool wide = b.k1 > kNarrowK1Bits;
-#define SCT_BIG(C, G, W)                                                                                          \
-  LAUNCH("big_bucket", (k_big_bucket<C, G, W>), bgrid, dim3(kBigBlock), s, (const Seg*)bigs, pa, pb, b, \
-         partials, dflags)
-    if (cell && gene) {
-      if (wide) { SCT_BIG(true, true, true); } else { SCT_BIG(true, true, false); }
-    } else if (cell) {
-      if (wide) { SCT_BIG(true, false, true); } else { SCT_BIG(true, false, false); }
-    } else {
-      if (wide) { SCT_BIG(false, false, true); } else { SCT_BIG(false, false, false); }
-    }
-#undef SCT_BIG
+  // 5.26 ms either way, profiles/r04/e_l1fast_gbam_dicts/var/); round 6: those of levels 0-1 already
+  // run beside levels >= 2 (above), so only the later levels' big buckets are launched here
+  if (early_big && !join_first) HIPCHK(side.to_caller(s));
+  if (h.n_big > big_done) {
+    rc = launch_big(h.n_big - big_done, bigs + big_done, s);
+    if (rc) return rc;
   }
   if (h.n_giant > 0) {
     const dim3 ggrid(h.n_giant);
@@ -680,13 +760,34 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     if (rc) return rc;
   }
 
+  // Round 6: a side stream forked after the key pass (planned bucket path, exact floats) runs the
+  // gene view's plan and the big buckets of levels 0-1 beside the partition levels >= 2 and the
+  // hash tiles, and the cell rows' finalize beside the gene view
+  SideStream side;
+  hipEvent_t plan_done = nullptr;
+  const char* no_side = getenv("SCT_NO_SIDE");
+  const bool use_side = bucket && planned && exact && !(no_side && no_side[0] == '1');
+  uint32_t* gcur = gene ? at<uint32_t>(ws, L.gcursor) : nullptr;
+  int64_t* gwork = gene ? at<int64_t>(ws, L.gwork) : nullptr;
+  int64_t* n_gwork = at<int64_t>(ws, L.scalars) + 4;
+  if (use_side) {
+    HIPCHK(side.open(s));
+    if (gene) {
+      LAUNCH_SHM("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), 2 * sizeof(uint32_t) * (size_t)(L.n_buckets + 1),
+                 side.use(), (const uint32_t*)gcounts, L.n_buckets, gcur, gwork, n_gwork);
+      HIPCHK(side.event(&plan_done));
+      HIPCHK(hipEventRecord(plan_done, side.s));
+    }
+  }
+
   // 2-3. distinct counts (+ per-record distinct events for the gene view)
   uint16_t* dflags = gene ? at<uint16_t>(ws, L.dflags) : nullptr;
   if (bucket) {
-    rc = bucket_distinct(L, ws, n, n_ent, ent_start, mito, b, cell, gene, partials, dflags, planned, s);
+    rc = bucket_distinct(L, ws, n, n_ent, ent_start, mito, b, cell, gene, partials, dflags, planned, s, side);
     if (rc == 1) {  // a mapped ref id does not fit the bucket payload: redo on the global-sort path
       if (wf.s2) HIPCHK(hipStreamSynchronize(wf.s2));  // (its workspace is reused by the redo)
       if (wf.s3) HIPCHK(hipStreamSynchronize(wf.s3));
+      if (side.is_open()) HIPCHK(hipStreamSynchronize(side.s));
       return pipeline(plan, rec, gene_is_mito, ws, ws_bytes, out_i, out_f, capacity, n_rows, gene_partials, s,
                       false);
     }
@@ -711,7 +812,11 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   }
 
   if (out_i) {
-    LAUNCH("finalize", k_finalize, dim3((unsigned)cdiv(n_ent * kFinThreads, kBlock)), dim3(kBlock), s, (const int64_t*)partials,
+    const char* no_sfin = getenv("SCT_NO_SIDE_FIN");
+    const bool side_fin = side.is_open() && gene && !(no_sfin && no_sfin[0] == '1');
+    if (side_fin) HIPCHK(side.from_caller(s));
+    hipStream_t fs = side_fin ? side.use() : s;
+    LAUNCH("finalize", k_finalize, dim3((unsigned)cdiv(n_ent * kFinThreads, kBlock)), dim3(kBlock), fs, (const int64_t*)partials,
            n_ent, cell ? SCT_MODE_CELL : SCT_MODE_GENE, exact ? 1 : 0, (const int64_t*)ent_start, out_i, out_f);
     if (!exact) {  // launched on the side streams after the key pass (welford_stage): joined here
       HIPCHK(hipEventRecord(wf.join, wf.s2));
@@ -722,12 +827,13 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   }
   if (gene) {
     // 4. gene view: bucket starts, payload emission (input order), bucket reduction
-    uint32_t* gcur = at<uint32_t>(ws, L.gcursor);
-    int64_t* gwork = at<int64_t>(ws, L.gwork);
-    int64_t* n_gwork = at<int64_t>(ws, L.scalars) + 4;
     void* gpay = at<GenePayload>(ws, L.gpay);
-    LAUNCH_SHM("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), 2 * sizeof(uint32_t) * (size_t)(L.n_buckets + 1), s,
-               (const uint32_t*)gcounts, L.n_buckets, gcur, gwork, n_gwork);
+    if (plan_done) {
+      HIPCHK(hipStreamWaitEvent(s, plan_done, 0));
+    } else {
+      LAUNCH_SHM("gene_plan", k_gene_plan, dim3(1), dim3(kBlock), 2 * sizeof(uint32_t) * (size_t)(L.n_buckets + 1), s,
+                 (const uint32_t*)gcounts, L.n_buckets, gcur, gwork, n_gwork);
+    }
     static_assert(kEmitTile == kKTile, "gene_emit tiles are the key pass's tiles (gtoff)");
     const int staged = L.n_buckets <= kEmitStagedBuckets ? 1 : 0;
     LAUNCH_SHM_N("gene_emit", n, k_gene_emit, dim3((unsigned)cdiv(n, kEmitTile)), dim3(kBlock),
@@ -736,6 +842,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
     LAUNCH_N("gene_reduce", n, k_gene_reduce, dim3((unsigned)L.max_gene_work), dim3(kBlock), s, (const void*)gpay,
            (const int64_t*)gwork, (const int64_t*)n_gwork, plan->n_gene_ids, (const uint32_t*)gwide, gene_partials);
   }
+  if (side.is_open()) HIPCHK(side.to_caller(s));
   if (n_rows) *n_rows = n_ent;
   return SCT_OK;
 }
