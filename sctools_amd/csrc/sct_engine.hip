@@ -163,8 +163,9 @@ int check_plan(const sct_plan_t* plan, const sct_records_t* rec) {
 
 // heads + scan of the entity column; with `dup_check`, also flags cell ids seen in two runs.
 // Copies (n_entities, dup flag) to the host and synchronizes.
+// pre: a fill queued behind the count's copy (round 6: it runs while the host waits for the count)
 int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool dup_check, int32_t n_ids,
-               int64_t* n_ent, bool* dup, hipStream_t s) {
+               int64_t* n_ent, bool* dup, hipStream_t s, FillBatch* pre = nullptr) {
   const int64_t tiles = cdiv(n, kTile);
   uint64_t* tc = at<uint64_t>(ws, L.tile_cnt);
   uint64_t* sc = at<uint64_t>(ws, L.scalars);
@@ -183,7 +184,13 @@ int count_runs(const int32_t* ent, int64_t n, void* ws, const Layout& L, bool du
   }
   LAUNCH("scan", k_scan_wide, dim3(1), dim3(kScanWide), s, tc, tiles, sc);
   uint64_t host[2] = {0, 0};
-  if (int rb = readback(host, sc, sizeof(host), s)) return rb;
+  if (pre) {
+    if (int rb = readback_start(sc, sizeof(host), s)) return rb;
+    if (int rc = launch_fills(*pre, s)) return rc;
+    if (int rb = readback_finish(host, sizeof(host))) return rb;
+  } else {
+    if (int rb = readback(host, sc, sizeof(host), s)) return rb;
+  }
   *n_ent = (int64_t)host[0];
   if (dup) *dup = host[1] & 1;
   if (host[1] & 2) return fail(SCT_EINVAL, "an entity id lies outside [0, %d)", n_ids);
@@ -212,8 +219,9 @@ int launch_hash_tile(bool cell, bool gene, dim3 grid, hipStream_t s, const uint1
 // segments there can be (the device count bounds it): l1.hist then holds every segment child's start.
 // No host wait.
 // (its buffers -- bdesc, the level-0 counters, l1.hist -- are zeroed by the caller: level1_fills)
-void level1_fills(const Layout& L, void* ws, int64_t n, int64_t n_ent, const L1Plan& l1, FillBatch& fb) {
-  fb.add(at<uint16_t>(ws, L.bdesc), sizeof(uint16_t) * (size_t)n);
+void level1_fills(const Layout& L, void* ws, int64_t n, int64_t n_ent, const L1Plan& l1, FillBatch& fb,
+                  bool bdesc_done) {
+  if (!bdesc_done) fb.add(at<uint16_t>(ws, L.bdesc), sizeof(uint16_t) * (size_t)n);
   fb.add(level0_ctr(ws, L), 3 * sizeof(uint32_t));
   fb.add(l1.hist, sizeof(uint32_t) * kRadix * (size_t)n_ent);
 }
@@ -370,7 +378,9 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
     return SCT_OK;
   };
   const char* no_early = getenv("SCT_NO_EARLY_BIG");
-  const bool early_big = side.is_open() && h.n_big > 0 && h.n_seg > 0 && !(no_early && no_early[0] == '1');
+  const bool side_big = side.is_open() && !(no_early && no_early[0] == '1');
+  const bool early_big = side_big && h.n_big > 0 && h.n_seg > 0;
+  const char* no_late = getenv("SCT_NO_LEVEL_BIG");
   uint32_t big_done = 0;
   if (early_big) {
     if (int r = launch_big(h.n_big, bigs, side.use())) return r;
@@ -402,6 +412,12 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
       err_pending = false;
       if (int e = err_check()) return e;
     }
+    // this level's big buckets (written by its scatter) join the side stream when another level follows
+    if (side_big && h.n_seg > 0 && h.n_big > big_done && !(no_late && no_late[0] == '1')) {
+      HIPCHK(side.from_caller(s));
+      if (int r = launch_big(h.n_big - big_done, bigs + big_done, side.use())) return r;
+      big_done = h.n_big;
+    }
     c ^= 1;
     depth += bits;
     level++;
@@ -410,7 +426,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   // the early big buckets finish before the hash tiles start (SCT_BIG_BESIDE_HASH=1: they may run into
   // them; the hash tiles' 40 KB blocks then hold every CU's LDS and the big buckets' 80 KB blocks wait)
   const char* beside = getenv("SCT_BIG_BESIDE_HASH");
-  const bool join_first = early_big && !(beside && beside[0] == '1');
+  const bool join_first = big_done > 0 && !(beside && beside[0] == '1');
   if (join_first) HIPCHK(side.to_caller(s));
   int rc;
   if (b.k1 > kNarrowK1Bits) {
@@ -422,7 +438,7 @@ int bucket_distinct(const Layout& L, void* ws, int64_t n, int64_t n_ent, const i
   // (round 4: the big buckets on a side stream beside the hash tiles measured the same step time,
   // 5.26 ms either way, profiles/r04/e_l1fast_gbam_dicts/var/); round 6: those of levels 0-1 already
   // run beside levels >= 2 (above), so only the later levels' big buckets are launched here
-  if (early_big && !join_first) HIPCHK(side.to_caller(s));
+  if (big_done > 0 && !join_first) HIPCHK(side.to_caller(s));
   if (h.n_big > big_done) {
     rc = launch_big(h.n_big - big_done, bigs + big_done, s);
     if (rc) return rc;
@@ -634,7 +650,18 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
 
   int64_t n_ent = 0;
   bool dup = false;
-  int rc = count_runs(ent_col, n, ws, L, gene, plan->n_cell_ids, &n_ent, &dup, s);
+  // the bucket descriptors (2 bytes per record, the step's largest fill) are zeroed while the host
+  // waits for the entity count, when the first partition level will be planned (below)
+  const char* nol1 = getenv("SCT_NO_L1_PLAN");
+  const char* force = getenv("SCT_FORCE_GLOBAL_SORT");
+  const char* nopre = getenv("SCT_NO_PREFILL");
+  const int k1_bits = bitlen((uint64_t)(cell ? plan->n_gene_ids : plan->n_cell_ids));
+  const bool may_plan = allow_bucket && k1_bits + bitlen((uint64_t)plan->n_umi_ids) <= kMaxKeyBits &&
+                        !(force && force[0] == '1') && L.max_ent <= kEntHistMax && k1_bits >= kRadixBits &&
+                        !(nol1 && nol1[0] == '1') && !(nopre && nopre[0] == '1') && n > 0;
+  FillBatch pre;
+  if (may_plan) pre.add(at<uint16_t>(ws, L.bdesc), sizeof(uint16_t) * (size_t)n);
+  int rc = count_runs(ent_col, n, ws, L, gene, plan->n_cell_ids, &n_ent, &dup, s, may_plan ? &pre : nullptr);
   if (rc) return rc;
   if (dup) return fail(SCT_EINVAL, "grouped gene partials need cell-sorted records (a cell id forms two runs)");
   if (n_ent > L.max_ent)
@@ -647,7 +674,6 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   Bits b;
   b.k1 = bitlen((uint64_t)(cell ? plan->n_gene_ids : plan->n_cell_ids));
   b.k2 = bitlen((uint64_t)plan->n_umi_ids);
-  const char* force = getenv("SCT_FORCE_GLOBAL_SORT");
   const bool bucket = allow_bucket && b.k1 + b.k2 <= kMaxKeyBits && !(force && force[0] == '1');
   int used;
   if (bucket) {
@@ -684,7 +710,6 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   uint32_t* gtoff = gene ? at<uint32_t>(ws, L.gtoff) : nullptr;
   // bucket path: the first partition level planned before the key pass when its digit comes from
   // k1 alone (segment.h k_level1_plan), so the key pass writes the level-1 children itself
-  const char* nol1 = getenv("SCT_NO_L1_PLAN");
   const bool planned = bucket && L.max_ent <= kEntHistMax && n_ent > 0 && b.k1 >= kRadixBits &&
                        !(nol1 && nol1[0] == '1');
   L1Plan l1{};
@@ -716,7 +741,7 @@ int pipeline(const sct_plan_t* plan, const sct_records_t* rec, const uint8_t* ge
   // pass; without it the wide format is used)
   uint32_t* gwide = reinterpret_cast<uint32_t*>(at<uint64_t>(ws, L.scalars) + 16);
   fb.add(gwide, sizeof(uint32_t), streams ? 0 : 1);
-  if (planned) level1_fills(L, ws, n, n_ent, l1, fb);
+  if (planned) level1_fills(L, ws, n, n_ent, l1, fb, may_plan);
   rc = launch_fills(fb, s);
   if (rc) return rc;
   if (planned) {

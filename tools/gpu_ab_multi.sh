@@ -23,7 +23,7 @@ for ((i = ${#V[@]} - 1; i >= 0; i--)); do ORDER+=("${V[$i]}:2"); done
 for ov in "${ORDER[@]}"; do
   nv=${ov%:*}; r=${ov##*:}
   name=${nv%%=*}; env=${nv#*=}
-  if [ "$name" == "tree" ]; then E=""; else E="env $env"; fi
+  if [ "$name" == "tree" ]; then E=""; else E="env ${env//,/ }"; fi
   timeout -k 10 300 $E python bench.py --no-cpu-baseline $ARGS > $OUT/bench_${name}_$r.json 2> $OUT/bench_${name}_$r.err || { tail -30 $OUT/bench_${name}_$r.err; exit 1; }
   python -c "import json; d=json.load(open('$OUT/bench_${name}_$r.json')); k=d['kernel_ms_per_step']; print('${name}_$r', 'ms/step %.3f' % d['ms_per_step'], {x: k[x] for x in list(k)[:6]})"
 done
