@@ -283,3 +283,55 @@ def test_reference_ids_beyond_the_payload_fall_back_to_the_global_sort(eng):
     assert any(k.startswith("radix") for k in ran), ran
     oi, of = O.run(arrays, "cell", mito, 300, threads=8)
     compare(out["i"].cpu().numpy(), out["f"].cpu().numpy(), oi, of, exact=True)
+
+
+# Round 6: the side stream after the key pass (big buckets beside the partition levels, the gene
+# view's plan, the cell rows' finalize) and the bucket-descriptor fill behind the entity count only
+# reorder work between streams: every switch must leave the rows bit-identical.
+SIDE_SWITCHES = [
+    {"SCT_NO_SIDE": "1", "SCT_NO_PREFILL": "1"},
+    {"SCT_NO_LEVEL_BIG": "1"},
+    {"SCT_NO_EARLY_BIG": "1"},
+    {"SCT_NO_SIDE_FIN": "1"},
+    {"SCT_BIG_BESIDE_HASH": "1"},
+]
+
+
+def _same_rows(a, b):
+    for k in a:
+        assert np.array_equal(a[k][0], b[k][0]), k
+        assert np.array_equal(np.nan_to_num(a[k][1], nan=7.0).view(np.int64),
+                              np.nan_to_num(b[k][1], nan=7.0).view(np.int64)), k
+
+
+@pytest.mark.parametrize("switches", SIDE_SWITCHES, ids=lambda d: ",".join(d))
+def test_side_stream_switches_leave_rows_identical(eng, monkeypatch, switches):
+    arrays, mito, n_cells = craft(30_000, 1 << 20, 6)
+    a = run_all(eng, arrays, mito, n_cells, 30_000, 1 << 20)
+    for k, v in switches.items():
+        monkeypatch.setenv(k, v)
+    b = run_all(eng, arrays, mito, n_cells, 30_000, 1 << 20)
+    _same_rows(a, b)
+
+
+def test_side_stream_switches_on_a_config2_shaped_shard(eng, monkeypatch):
+    """4M config-2-shaped records (Zipf genes, ~10k-record cells): partition levels 2-3, big buckets
+    from several levels, so the side stream carries work at every level."""
+    from sctools_amd import engine as E
+    from sctools_amd import synth
+
+    d = synth.generate(synth.SynthConfig(n_reads=4_000_000, n_cells=400, n_genes=30_000, seed=11),
+                       device=eng.device, chunk=16_000_000)
+    dims = E.Dims(d.n_cell_ids, d.n_gene_ids, d.n_umi_ids)
+    mito = torch.from_numpy(d.gene_is_mito).to(eng.device)
+
+    def rows():
+        ci, cf, part = eng.cell_and_gene(d.cols, dims, mito)
+        gi, gf = eng.finalize_partials(part)
+        return {"cell": (ci.cpu().numpy(), cf.cpu().numpy()), "gene": (gi.cpu().numpy(), gf.cpu().numpy())}
+
+    a = rows()
+    monkeypatch.setenv("SCT_NO_SIDE", "1")
+    monkeypatch.setenv("SCT_NO_PREFILL", "1")
+    b = rows()
+    _same_rows(a, b)
